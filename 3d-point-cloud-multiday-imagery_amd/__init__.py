@@ -1,0 +1,32 @@
+"""MI355X-native multi-day point-cloud K-means (Lloyd) reconstruction step.
+
+Drop-in for the K-means step of the ``members/rafael`` "Multi-day 3D Point
+Cloud" plugin (see DESIGN.md / INTEGRATION.md).  Import name: ``pcm_amd``
+(the repository-root shim ``pcm_amd.py`` maps it onto this directory).
+
+Public API
+----------
+lloyd_fit(X, centers_init, max_iter, tol, group=None)  -> LloydResult
+kmeans_fuse(clouds, n_clusters, ...)                   -> napari layer tuples
+HeightMapExtractor                                     -> SatellitePlugin drop-in
+Engine                                                 -> the C-ABI engine wrapper
+"""
+from .fixed import QBITS, fixed_q  # noqa: F401
+from .lloyd import LloydResult, lloyd_fit  # noqa: F401
+
+__all__ = ["lloyd_fit", "LloydResult", "fixed_q", "QBITS", "Engine", "kmeans_fuse", "HeightMapExtractor",
+           "build_library"]
+
+
+def __getattr__(name):
+    # lazy: the engine needs torch + the HIP library, the plugin needs neither at import
+    if name == "Engine":
+        from .engine import Engine
+        return Engine
+    if name in ("kmeans_fuse", "HeightMapExtractor", "PREFIX"):
+        from . import plugin
+        return getattr(plugin, name)
+    if name == "build_library":
+        from ._lib import build
+        return build
+    raise AttributeError(name)

@@ -1,0 +1,123 @@
+"""Loader and build recipe of the C-ABI HIP library ``libpcmkm.so``.
+
+The library is built in-tree (``build()``), so the shared object travels with
+the repository snapshot to the GPU box.  ``load()`` fails loudly when the
+library is missing: there is no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+SO_PATH = os.environ.get("PCM_SO") or os.path.join(PKG_DIR, "libpcmkm.so")
+SOURCES = [os.path.join(PKG_DIR, "csrc", "pcm_engine.hip"), os.path.join(PKG_DIR, "csrc", "pcm_kernels.hpp"),
+           os.path.join(REPO_DIR, "include", "pcm_kmeans.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
+
+# Every symbol include/pcm_kmeans.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "pcm_abi_version", "pcm_last_error", "pcm_engine_create", "pcm_engine_destroy", "pcm_layout_bbox",
+    "pcm_layout_build", "pcm_fit_begin", "pcm_iter_local", "pcm_iter_global", "pcm_iterate", "pcm_stats_ptr",
+    "pcm_bind_stats", "pcm_reloc_candidates", "pcm_reloc_apply", "pcm_final", "pcm_labels", "pcm_get_centers",
+    "pcm_history", "pcm_read_status", "pcm_layout_info", "pcm_candidate_stats", "pcm_synth_uniform",
+    "pcm_assign_bruteforce", "pcm_timing", "pcm_timing_read", "pcm_synth_rows",
+]
+
+_lock = threading.Lock()
+_lib = None
+
+
+class PcmError(RuntimeError):
+    pass
+
+
+class PcmStatus(ctypes.Structure):
+    _fields_ = [("halt", ctypes.c_uint32), ("done", ctypes.c_uint32), ("iter", ctypes.c_uint32),
+                ("n_empty", ctypes.c_uint32), ("inertia", ctypes.c_double), ("last_changed", ctypes.c_uint64),
+                ("last_shift", ctypes.c_double)]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(SO_PATH):
+        return True
+    t = os.path.getmtime(SO_PATH)
+    return any(os.path.getmtime(s) > t for s in SOURCES if os.path.exists(s))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile ``libpcmkm.so`` for gfx950 with hipcc (works without a GPU)."""
+    if not force and not needs_build():
+        return SO_PATH
+    cmd = [HIPCC, *HIP_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-o", SO_PATH + ".tmp", SOURCES[0]]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(SO_PATH + ".tmp", SO_PATH)
+    return SO_PATH
+
+
+def _declare(lib):
+    P, I, I64, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    sig = {
+        "pcm_abi_version": ([], I),
+        "pcm_last_error": ([ctypes.c_char_p, ctypes.c_size_t], I),
+        "pcm_engine_create": ([I, I, I, I, I, ctypes.POINTER(P)], I),
+        "pcm_engine_destroy": ([P], I),
+        "pcm_layout_bbox": ([P, P, I64, P, P, P, P], I),
+        "pcm_layout_build": ([P, P, P, I64, P], I),
+        "pcm_fit_begin": ([P, P, D, I, P], I),
+        "pcm_iter_local": ([P, P], I),
+        "pcm_iter_global": ([P, P], I),
+        "pcm_iterate": ([P, I, P], I),
+        "pcm_stats_ptr": ([P, ctypes.POINTER(P), ctypes.POINTER(I64)], I),
+        "pcm_bind_stats": ([P, P], I),
+        "pcm_reloc_candidates": ([P, I, P, P], I),
+        "pcm_reloc_apply": ([P, P, I, P], I),
+        "pcm_final": ([P, P], I),
+        "pcm_labels": ([P, P, P], I),
+        "pcm_get_centers": ([P, P, P], I),
+        "pcm_history": ([P, P, P, I, P], I),
+        "pcm_read_status": ([P, ctypes.POINTER(PcmStatus), P], I),
+        "pcm_layout_info": ([P, ctypes.POINTER(I64), ctypes.POINTER(I64), P], I),
+        "pcm_candidate_stats": ([P, ctypes.POINTER(D), ctypes.POINTER(I), ctypes.POINTER(I64), P], I),
+        "pcm_synth_uniform": ([P, I64, I, ctypes.c_uint64, I64, P], I),
+        "pcm_assign_bruteforce": ([P, I64, I, P, I, P, P, P, P], I),
+        "pcm_timing": ([P, I], I),
+        "pcm_timing_read": ([P, P, ctypes.POINTER(I)], I),
+        "pcm_synth_rows": ([P, P, I64, I, ctypes.c_uint64, P], I),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+
+
+def load(require_gpu_runtime: bool = True):
+    """Load the library (after torch, so one HIP runtime serves both)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(SO_PATH):
+                raise PcmError(f"HIP extension missing: {SO_PATH} (run __graft_entry__.build())")
+            if require_gpu_runtime:
+                import torch  # noqa: F401  (loads torch's libamdhip64.so.7 first)
+            lib = ctypes.CDLL(SO_PATH)
+            _declare(lib)
+            _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(1024)
+    load().pcm_last_error(buf, 1024)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        raise PcmError(f"{what} failed ({rc}): {last_error()}")

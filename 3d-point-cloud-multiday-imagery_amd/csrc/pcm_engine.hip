@@ -1,0 +1,798 @@
+// pcm_engine.hip — host runtime + C ABI (include/pcm_kmeans.h) of the MI355X
+// multi-day point-cloud Lloyd engine.  All device work is stream-ordered; the
+// per-iteration entry points allocate nothing and never synchronise, so a
+// caller may capture them into a HIP graph.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "pcm_kernels.hpp"
+#include "pcm_kmeans.h"
+
+using namespace pcm;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace
+
+#define HIPCHK(expr)                                                                             \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            return fail(PCM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e) + " @" +   \
+                                       std::to_string(__LINE__));                               \
+    } while (0)
+
+#define LAUNCHCHK() HIPCHK(hipGetLastError())
+
+struct pcm_engine {
+    int device = 0, d = 3, k = 1, dtype = PCM_F32, max_iter_cap = 300;
+    long long n = 0, npad = 0, gidx0 = 0;
+    double lo[MAXD] = {0}, hi[MAXD] = {0}, maxabs[MAXD] = {0};
+    bool have_bbox = false, layout_ready = false, fit_ready = false;
+    Grid g{};
+    QExp qe{};
+    long long ntiles = 0;
+    // device buffers
+    void *xs = nullptr;
+    uint32_t *perm = nullptr;
+    int32_t *lab = nullptr;
+    uint32_t *cell_start = nullptr;
+    uint32_t *tile_off = nullptr;    // [ncells+1] first tile of each cell
+    uint4 *tiles = nullptr;
+    int num_cu = 256;
+    uint32_t *cc_cnt = nullptr, *cc_idx = nullptr, *fc_cnt = nullptr;
+    float4 *fc_rec = nullptr;
+    int32_t *fc_lab = nullptr;
+    float4 *C = nullptr, *Cn = nullptr;
+    unsigned long long *partials = nullptr, *stats = nullptr, *hist_changed = nullptr;
+    unsigned long long *stats_own = nullptr;   // engine-owned; `stats` may point at a bound buffer
+    unsigned long long *held = nullptr;        // statistics of a halted iteration
+    double *hist_shift = nullptr;
+    Ctrl *ctrl = nullptr;
+    float *bbox_part = nullptr;
+    unsigned *nonfinite = nullptr;
+    double *bbox_out = nullptr;
+    unsigned long long *cand_stats = nullptr;
+    int *rank_buf = nullptr;
+    int rank_cap = 0;
+    Ctrl ctrl_host{};
+    // optional kernel timing: event pairs per iteration, summed on read
+    static constexpr int TEV = 64;
+    bool timing = false;
+    hipEvent_t ev[TEV][4] = {};
+    int ev_next = 0, ev_pending = 0;
+    double t_sum[3] = {0, 0, 0};
+    long long t_count = 0;
+};
+
+namespace {
+
+const int BBOX_BLOCKS = 1024;
+
+size_t tsize(int dtype) { return dtype == PCM_F16 ? 2 : 4; }
+
+int check_device(pcm_engine *e) {
+    int cur = -1;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != e->device)
+        return fail(PCM_E_STATE, "current HIP device " + std::to_string(cur) + " != engine device " +
+                                     std::to_string(e->device));
+    return 0;
+}
+
+template <typename F>
+int dispatch_d(int d, F &&f) {
+    switch (d) {
+        case 1: return f(std::integral_constant<int, 1>{});
+        case 2: return f(std::integral_constant<int, 2>{});
+        case 3: return f(std::integral_constant<int, 3>{});
+        case 4: return f(std::integral_constant<int, 4>{});
+    }
+    return fail(PCM_E_ARG, "d must be 1..4");
+}
+
+template <typename F>
+int dispatch_td(int dtype, int d, F &&f) {
+    if (dtype == PCM_F16)
+        return dispatch_d(d, [&](auto DD) { return f(__half{}, DD); });
+    return dispatch_d(d, [&](auto DD) { return f(float{}, DD); });
+}
+
+void free_layout(pcm_engine *e) {
+    void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->cc_cnt, e->cc_idx,
+                  e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
+    e->tile_off = nullptr;
+    e->cc_cnt = nullptr; e->cc_idx = nullptr; e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
+    e->layout_ready = false;
+    e->fit_ready = false;
+}
+
+// Choose the pruning grid: about min(32 K, n / 1024) roughly cubic cells over
+// the bounding box (degenerate axes get one cell).
+void choose_grid(pcm_engine *e) {
+    Grid &g = e->g;
+    g = Grid{};
+    g.d = e->d;
+    g.F = 4;
+    double target = std::min(32.0 * e->k, (double)e->n / 1024.0);
+    target = std::max(1.0, std::min(target, (double)(1 << 18)));
+    double vol = 1.0;
+    int nondeg = 0;
+    double maxext = 0.0;
+    for (int a = 0; a < MAXD; ++a) {
+        g.G[a] = 1;
+        g.GC[a] = 1;
+    }
+    for (int a = 0; a < e->d; ++a) {
+        double ex = e->hi[a] - e->lo[a];
+        g.ext[a] = ex;
+        g.lo[a] = e->lo[a];
+        maxext = std::max(maxext, ex);
+        if (ex > 0) {
+            vol *= ex;
+            nondeg++;
+        }
+    }
+    if (nondeg > 0) {
+        double s = std::pow(vol / target, 1.0 / nondeg);
+        for (int a = 0; a < e->d; ++a) {
+            if (g.ext[a] > 0) {
+                long long G = std::llround(g.ext[a] / s);
+                g.G[a] = (int)std::max(1LL, std::min(G, 4096LL));
+            }
+        }
+    }
+    long long nc = 1;
+    for (int a = 0; a < e->d; ++a) nc *= g.G[a];
+    while (nc > (1LL << 20)) {   // keep keys and candidate tables bounded
+        int amax = 0;
+        for (int a = 1; a < e->d; ++a)
+            if (g.G[a] > g.G[amax]) amax = a;
+        g.G[amax] = std::max(1, g.G[amax] / 2);
+        nc = 1;
+        for (int a = 0; a < e->d; ++a) nc *= g.G[a];
+    }
+    long long ncc = 1;
+    for (int a = 0; a < e->d; ++a) {
+        g.w[a] = g.ext[a] / g.G[a];
+        g.inv[a] = g.ext[a] > 0 ? (double)g.G[a] / g.ext[a] : 0.0;
+        g.mg[a] = 1e-7 * g.ext[a];
+        g.GC[a] = (g.G[a] + g.F - 1) / g.F;
+        ncc *= g.GC[a];
+    }
+    g.ncells = nc;
+    g.ncoarse = ncc;
+    // fp32 distances overflow beyond ~1.8e19: no pruning then (brute force is exact)
+    g.prune = (maxext < 1e18 && e->k > 1) ? 1 : 0;
+}
+
+int blocks_for(long long n, int bs = 256) { return (int)std::max(1LL, (n + bs - 1) / bs); }
+
+}  // namespace
+
+extern "C" {
+
+int pcm_abi_version(void) { return PCM_ABI_VERSION; }
+
+int pcm_last_error(char *buf, size_t n) {
+    if (!buf || n == 0) return PCM_E_ARG;
+    std::snprintf(buf, n, "%s", g_err.c_str());
+    return 0;
+}
+
+int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_engine **out) {
+    if (!out) return fail(PCM_E_ARG, "out is null");
+    *out = nullptr;
+    if (d < 1 || d > MAXD) return fail(PCM_E_ARG, "d must be 1..4");
+    if (k < 1 || k > (1 << 20)) return fail(PCM_E_ARG, "k out of range");
+    if (dtype != PCM_F32 && dtype != PCM_F16) return fail(PCM_E_ARG, "dtype must be PCM_F32 or PCM_F16");
+    if (max_iter < 1) return fail(PCM_E_ARG, "max_iter must be >= 1");
+    pcm_engine *e = new pcm_engine();
+    e->device = device;
+    e->d = d;
+    e->k = k;
+    e->dtype = dtype;
+    e->max_iter_cap = max_iter;
+    int rc = check_device(e);
+    if (rc) { delete e; return rc; }
+    if (hipDeviceGetAttribute(&e->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        e->num_cu < 1)
+        e->num_cu = 256;
+    const size_t nstat = (size_t)k * (d + 1) + 1;
+    hipError_t err = hipSuccess;
+    err = err ? err : hipMalloc(&e->C, (size_t)k * sizeof(float4));
+    err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
+    err = err ? err : hipMalloc(&e->partials, (size_t)NREP * k * (d + 1) * sizeof(unsigned long long));
+    err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
+    e->stats = e->stats_own;
+    err = err ? err : hipMalloc(&e->held, nstat * sizeof(unsigned long long));
+    err = err ? err : hipMalloc(&e->hist_changed, (size_t)max_iter * sizeof(unsigned long long));
+    err = err ? err : hipMalloc(&e->hist_shift, (size_t)max_iter * sizeof(double));
+    err = err ? err : hipMalloc(&e->ctrl, sizeof(Ctrl));
+    err = err ? err : hipMalloc(&e->bbox_part, (size_t)BBOX_BLOCKS * 2 * MAXD * sizeof(float));
+    err = err ? err : hipMalloc(&e->nonfinite, sizeof(unsigned));
+    err = err ? err : hipMalloc(&e->bbox_out, 2 * MAXD * sizeof(double));
+    err = err ? err : hipMalloc(&e->cand_stats, 3 * sizeof(unsigned long long));
+    err = err ? err : hipMemset(e->partials, 0, (size_t)NREP * k * (d + 1) * sizeof(unsigned long long));
+    err = err ? err : hipMemset(e->ctrl, 0, sizeof(Ctrl));
+    if (err != hipSuccess) {
+        pcm_engine_destroy(e);
+        return fail(PCM_E_NOMEM, std::string("engine allocation: ") + hipGetErrorString(err));
+    }
+    *out = e;
+    return 0;
+}
+
+int pcm_engine_destroy(pcm_engine *e) {
+    if (!e) return 0;
+    for (int i = 0; i < pcm_engine::TEV; ++i)
+        for (int j = 0; j < 4; ++j)
+            if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
+    free_layout(e);
+    void *ps[] = {e->C, e->Cn, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
+                  e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    delete e;
+    return 0;
+}
+
+int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream, double *lo, double *hi, double *maxabs) {
+    if (!e || (!X && n > 0) || n < 0 || !lo || !hi || !maxabs) return fail(PCM_E_ARG, "bad argument");
+    if (n >= (1LL << 32) - 8) return fail(PCM_E_ARG, "n must be < 2^32 per engine");
+    if (int rc = check_device(e)) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    e->n = n;
+    e->have_bbox = false;
+    free_layout(e);
+    if (n == 0) {
+        for (int a = 0; a < e->d; ++a) lo[a] = hi[a] = maxabs[a] = e->lo[a] = e->hi[a] = e->maxabs[a] = 0.0;
+        e->have_bbox = true;
+        return 0;
+    }
+    HIPCHK(hipMemsetAsync(e->nonfinite, 0, sizeof(unsigned), s));
+    int nblk = (int)std::min<long long>(BBOX_BLOCKS, (n + 255) / 256);
+    int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        k_bbox_partial<TT, D><<<nblk, 256, 0, s>>>((const TT *)X, n, e->bbox_part, e->nonfinite);
+        LAUNCHCHK();
+        k_bbox_final<D><<<1, 64, 0, s>>>(e->bbox_part, nblk, e->bbox_out);
+        LAUNCHCHK();
+        return 0;
+    });
+    if (rc) return rc;
+    double hb[2 * MAXD];
+    unsigned nf = 0;
+    HIPCHK(hipMemcpyAsync(hb, e->bbox_out, 2 * e->d * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nf, e->nonfinite, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (nf) return fail(PCM_E_NONFINITE, "input points contain NaN or Inf");
+    for (int a = 0; a < e->d; ++a) {
+        e->lo[a] = lo[a] = hb[a];
+        e->hi[a] = hi[a] = hb[e->d + a];
+        e->maxabs[a] = maxabs[a] = std::max(std::fabs(hb[a]), std::fabs(hb[e->d + a]));
+    }
+    e->have_bbox = true;
+    return 0;
+}
+
+int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gidx0, void *stream) {
+    if (!e || !q) return fail(PCM_E_ARG, "bad argument");
+    if (!e->have_bbox) return fail(PCM_E_STATE, "pcm_layout_bbox must run first");
+    if (int rc = check_device(e)) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    free_layout(e);
+    for (int a = 0; a < MAXD; ++a) e->qe.q[a] = a < e->d ? q[a] : 0;
+    e->gidx0 = gidx0;
+    const long long n = e->n;
+    e->npad = ((n + 3) / 4) * 4 + 4;
+    choose_grid(e);
+    const long long nc = e->g.ncells, ncc = e->g.ncoarse;
+    const size_t ts = tsize(e->dtype);
+
+    HIPCHK(hipMalloc(&e->xs, (size_t)e->d * e->npad * ts));
+    HIPCHK(hipMalloc(&e->lab, (size_t)e->npad * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&e->perm, (size_t)std::max(1LL, n) * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->cell_start, (size_t)(nc + 1) * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->cc_cnt, (size_t)ncc * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->cc_idx, (size_t)ncc * CAPC * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->fc_cnt, (size_t)nc * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->fc_rec, (size_t)nc * CAPF * sizeof(float4)));
+    HIPCHK(hipMalloc(&e->fc_lab, (size_t)nc * CAPF * sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(e->fc_cnt, 0, (size_t)nc * sizeof(uint32_t), s));
+
+    if (n == 0) {
+        HIPCHK(hipMalloc(&e->tile_off, (size_t)(nc + 1) * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(e->tile_off, 0, (size_t)(nc + 1) * sizeof(uint32_t), s));
+        HIPCHK(hipMemsetAsync(e->cell_start, 0, (size_t)(nc + 1) * sizeof(uint32_t), s));
+        HIPCHK(hipMemsetAsync(e->lab, 0xff, (size_t)e->npad * sizeof(int32_t), s));
+        HIPCHK(hipMemsetAsync(e->xs, 0, (size_t)e->d * e->npad * ts, s));
+        e->ntiles = 0;
+        HIPCHK(hipStreamSynchronize(s));
+        e->layout_ready = true;
+        return 0;
+    }
+
+    uint32_t *keys = nullptr, *keys2 = nullptr, *vals = nullptr, *tcnt = nullptr;
+    void *tmp = nullptr;
+    size_t tmp_bytes = 0, scan_bytes = 0;
+    auto cleanup = [&]() {
+        void *ps[] = {keys, keys2, vals, tcnt, tmp};
+        for (void *p : ps)
+            if (p) (void)hipFree(p);
+    };
+    int rc = 0;
+    do {
+        hipError_t err;
+        if ((err = hipMalloc(&keys, n * sizeof(uint32_t))) || (err = hipMalloc(&keys2, n * sizeof(uint32_t))) ||
+            (err = hipMalloc(&vals, n * sizeof(uint32_t))) || (err = hipMalloc(&tcnt, nc * sizeof(uint32_t))) ||
+            (err = hipMalloc(&e->tile_off, (nc + 1) * sizeof(uint32_t)))) {
+            rc = fail(PCM_E_NOMEM, std::string("layout scratch: ") + hipGetErrorString(err));
+            break;
+        }
+        unsigned bits = 1;
+        while ((1LL << bits) < nc) ++bits;
+        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+            using TT = decltype(T);
+            constexpr int D = decltype(DD)::value;
+            k_cellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, keys, vals);
+            LAUNCHCHK();
+            return 0;
+        });
+        if (rc) break;
+        if ((err = rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))) {
+            rc = fail(PCM_E_HIP, "radix_sort size query failed");
+            break;
+        }
+        uint32_t *toff = e->tile_off;
+        if ((err = rocprim::exclusive_scan(nullptr, scan_bytes, tcnt, toff, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s))) {
+            rc = fail(PCM_E_HIP, "scan size query failed");
+            break;
+        }
+        if ((err = hipMalloc(&tmp, std::max(tmp_bytes, scan_bytes)))) {
+            rc = fail(PCM_E_NOMEM, "sort scratch");
+            break;
+        }
+        size_t tb = tmp_bytes;
+        if ((err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))) {
+            rc = fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
+            break;
+        }
+        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+            using TT = decltype(T);
+            constexpr int D = decltype(DD)::value;
+            k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs, e->lab);
+            LAUNCHCHK();
+            return 0;
+        });
+        if (rc) break;
+        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, e->cell_start);
+        if ((err = hipGetLastError())) { rc = fail(PCM_E_HIP, "k_cell_starts"); break; }
+        k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt);
+        if ((err = hipGetLastError())) { rc = fail(PCM_E_HIP, "k_tile_counts"); break; }
+        size_t sb = scan_bytes;
+        if ((err = rocprim::exclusive_scan(tmp, sb, tcnt, toff, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s))) {
+            rc = fail(PCM_E_HIP, "scan");
+            break;
+        }
+        uint32_t last_off = 0, last_cnt = 0;
+        if ((err = hipMemcpyAsync(&last_off, toff + nc - 1, 4, hipMemcpyDeviceToHost, s)) ||
+            (err = hipMemcpyAsync(&last_cnt, tcnt + nc - 1, 4, hipMemcpyDeviceToHost, s)) ||
+            (err = hipStreamSynchronize(s))) {
+            rc = fail(PCM_E_HIP, std::string("tile count readback: ") + hipGetErrorString(err));
+            break;
+        }
+        e->ntiles = (long long)last_off + last_cnt;
+        {
+            uint32_t nt32 = (uint32_t)e->ntiles;
+            if ((err = hipMemcpy(toff + nc, &nt32, 4, hipMemcpyHostToDevice))) {
+                rc = fail(PCM_E_HIP, "tile_off tail");
+                break;
+            }
+        }
+        if ((err = hipMalloc(&e->tiles, (size_t)std::max(1LL, e->ntiles) * sizeof(uint4)))) {
+            rc = fail(PCM_E_NOMEM, "tiles");
+            break;
+        }
+        k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, toff, nc, e->tiles);
+        if ((err = hipGetLastError())) { rc = fail(PCM_E_HIP, "k_tile_write"); break; }
+        if ((err = hipStreamSynchronize(s))) { rc = fail(PCM_E_HIP, std::string("layout: ") + hipGetErrorString(err)); break; }
+    } while (0);
+    cleanup();
+    if (rc) {
+        free_layout(e);
+        return rc;
+    }
+    e->layout_ready = true;
+    return 0;
+}
+
+int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void *stream) {
+    if (!e || !C0) return fail(PCM_E_ARG, "bad argument");
+    if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
+    if (max_iter < 1 || max_iter > e->max_iter_cap) return fail(PCM_E_ARG, "max_iter exceeds the engine's cap");
+    if (!(tol >= 0.0)) return fail(PCM_E_ARG, "tol must be >= 0");
+    if (int rc = check_device(e)) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = dispatch_d(e->d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_centers_in<D><<<blocks_for(e->k), 256, 0, s>>>(C0, e->k, e->C);
+        LAUNCHCHK();
+        return 0;
+    });
+    if (rc) return rc;
+    k_fill_i32<<<blocks_for(e->npad), 256, 0, s>>>(e->lab, e->npad, -1);
+    LAUNCHCHK();
+    HIPCHK(hipMemsetAsync(e->partials, 0, (size_t)NREP * e->k * (e->d + 1) * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(e->hist_changed, 0, (size_t)e->max_iter_cap * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(e->hist_shift, 0, (size_t)e->max_iter_cap * sizeof(double), s));
+    e->ctrl_host = Ctrl{};
+    e->ctrl_host.max_iter = (uint32_t)max_iter;
+    e->ctrl_host.tol = tol;
+    HIPCHK(hipMemcpyAsync(e->ctrl, &e->ctrl_host, sizeof(Ctrl), hipMemcpyHostToDevice, s));
+    e->fit_ready = true;
+    return 0;
+}
+
+static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
+    return dispatch_d(e->d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_coarse<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->ctrl, gate);
+        LAUNCHCHK();
+        k_fine<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->fc_cnt, e->fc_rec,
+                                                    e->fc_lab, e->tile_off, e->tiles, e->ctrl, gate);
+        LAUNCHCHK();
+        return 0;
+    });
+}
+
+// Persistent grid: 4 resident 256-thread blocks per CU (LDS-limited), never
+// more blocks than tiles.
+static int assign_grid(pcm_engine *e) { return (int)std::min<long long>(e->ntiles, 4LL * e->num_cu); }
+
+static AssignArgs assign_args(pcm_engine *e) {
+    AssignArgs A{};
+    A.xs = e->xs;
+    A.npad = e->npad;
+    A.tiles = e->tiles;
+    A.ntiles = e->ntiles;
+    A.fc_rec = e->fc_rec;
+    A.fc_lab = e->fc_lab;
+    A.C = e->C;
+    A.K = e->k;
+    for (int a = 0; a < MAXD; ++a) A.q[a] = e->qe.q[a];
+    A.lab = e->lab;
+    A.partials = e->partials;
+    A.ctrl = e->ctrl;
+    return A;
+}
+
+// Fold completed event pairs into the sums (non-blocking unless the ring is full).
+static int timing_drain(pcm_engine *e, bool block) {
+    while (e->ev_pending > 0) {
+        int slot = (e->ev_next - e->ev_pending + pcm_engine::TEV) % pcm_engine::TEV;
+        if (block) HIPCHK(hipEventSynchronize(e->ev[slot][3]));
+        else if (hipEventQuery(e->ev[slot][3]) != hipSuccess) return 0;
+        float a = 0, b = 0, c = 0;
+        HIPCHK(hipEventElapsedTime(&a, e->ev[slot][0], e->ev[slot][1]));
+        HIPCHK(hipEventElapsedTime(&b, e->ev[slot][1], e->ev[slot][2]));
+        HIPCHK(hipEventElapsedTime(&c, e->ev[slot][2], e->ev[slot][3]));
+        e->t_sum[1] += a;   // candidates
+        e->t_sum[0] += b;   // assign
+        e->t_sum[2] += c;   // fold + global
+        e->t_count++;
+        e->ev_pending--;
+    }
+    return 0;
+}
+
+static int timing_mark(pcm_engine *e, int which, hipStream_t s) {
+    if (!e->timing) return 0;
+    if (which == 0) {
+        if (e->ev_pending == pcm_engine::TEV)
+            if (int rc = timing_drain(e, true)) return rc;
+        if (!e->ev[e->ev_next][0])
+            for (int j = 0; j < 4; ++j) HIPCHK(hipEventCreate(&e->ev[e->ev_next][j]));
+    }
+    HIPCHK(hipEventRecord(e->ev[e->ev_next][which], s));
+    if (which == 3) {
+        e->ev_next = (e->ev_next + 1) % pcm_engine::TEV;
+        e->ev_pending++;
+    }
+    return 0;
+}
+
+int pcm_iter_local(pcm_engine *e, void *stream) {
+    if (!e) return fail(PCM_E_ARG, "null engine");
+    if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
+    hipStream_t s = (hipStream_t)stream;
+    if (int rc = timing_mark(e, 0, s)) return rc;
+    if (int rc = launch_candidates(e, s, 1)) return rc;
+    if (int rc = timing_mark(e, 1, s)) return rc;
+    AssignArgs A = assign_args(e);
+    return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        if (e->ntiles > 0) {
+            const size_t lds = (size_t)MSLOT * (D + 1) * TPB * sizeof(uint32_t);
+            k_assign<TT, D, 0><<<assign_grid(e), TPB, lds, s>>>(A);
+            LAUNCHCHK();
+        }
+        if (int rc = timing_mark(e, 2, s)) return rc;
+        const int nf = e->k * (D + 1) + 1;
+        k_fold<D><<<blocks_for(nf), 256, 0, s>>>(e->partials, e->k, e->stats, e->ctrl);
+        LAUNCHCHK();
+        return 0;
+    });
+}
+
+int pcm_iter_global(pcm_engine *e, void *stream) {
+    if (!e) return fail(PCM_E_ARG, "null engine");
+    if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
+    hipStream_t s = (hipStream_t)stream;
+    return dispatch_d(e->d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_global<D><<<1, 1024, 0, s>>>(e->stats, e->k, e->qe, e->held, e->C, e->Cn, e->hist_changed, e->hist_shift,
+                                       e->ctrl);
+        LAUNCHCHK();
+        return timing_mark(e, 3, s);
+    });
+}
+
+int pcm_timing(pcm_engine *e, int enable) {
+    if (!e) return fail(PCM_E_ARG, "null engine");
+    if (int rc = timing_drain(e, true)) return rc;
+    e->timing = enable != 0;
+    e->t_sum[0] = e->t_sum[1] = e->t_sum[2] = 0.0;
+    e->t_count = 0;
+    return 0;
+}
+
+int pcm_timing_read(pcm_engine *e, double *ms, int *count) {
+    if (!e || !ms || !count) return fail(PCM_E_ARG, "bad argument");
+    if (int rc = timing_drain(e, true)) return rc;
+    for (int i = 0; i < 3; ++i) ms[i] = e->t_count ? e->t_sum[i] / (double)e->t_count : 0.0;
+    *count = (int)e->t_count;
+    return 0;
+}
+
+int pcm_iterate(pcm_engine *e, int n, void *stream) {
+    if (!e || n < 0) return fail(PCM_E_ARG, "bad argument");
+    for (int i = 0; i < n; ++i) {
+        if (int rc = pcm_iter_local(e, stream)) return rc;
+        if (int rc = pcm_iter_global(e, stream)) return rc;
+    }
+    return 0;
+}
+
+int pcm_stats_ptr(pcm_engine *e, void **ptr, int64_t *count) {
+    if (!e || !ptr || !count) return fail(PCM_E_ARG, "bad argument");
+    *ptr = e->stats;
+    *count = (int64_t)e->k * (e->d + 1) + 1;
+    return 0;
+}
+
+int pcm_bind_stats(pcm_engine *e, void *ptr) {
+    if (!e) return fail(PCM_E_ARG, "null engine");
+    e->stats = ptr ? (unsigned long long *)ptr : e->stats_own;
+    return 0;
+}
+
+int pcm_reloc_candidates(pcm_engine *e, int m, void *records, void *stream) {
+    if (!e || m < 1 || !records) return fail(PCM_E_ARG, "bad argument");
+    if (!e->fit_ready) return fail(PCM_E_STATE, "no fit in progress");
+    hipStream_t s = (hipStream_t)stream;
+    const long long n = e->n;
+    if (n == 0) {
+        HIPCHK(hipMemsetAsync(records, 0, (size_t)m * sizeof(RelocRec), s));
+        return 0;
+    }
+    unsigned long long *k1 = nullptr, *k2 = nullptr;
+    uint32_t *v1 = nullptr, *v2 = nullptr;
+    void *tmp = nullptr;
+    size_t tb = 0;
+    int rc = 0;
+    do {
+        hipError_t err;
+        if ((err = hipMalloc(&k1, n * 8)) || (err = hipMalloc(&k2, n * 8)) || (err = hipMalloc(&v1, n * 4)) ||
+            (err = hipMalloc(&v2, n * 4))) {
+            rc = fail(PCM_E_NOMEM, "reloc scratch");
+            break;
+        }
+        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+            using TT = decltype(T);
+            constexpr int D = decltype(DD)::value;
+            k_reloc_keys<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)e->xs, n, e->npad, e->lab, e->perm, e->C,
+                                                             e->gidx0, k1, v1);
+            LAUNCHCHK();
+            return 0;
+        });
+        if (rc) break;
+        if ((err = rocprim::radix_sort_pairs_desc(nullptr, tb, k1, k2, v1, v2, (size_t)n, 0u, 64u, s)) ||
+            (err = hipMalloc(&tmp, tb))) {
+            rc = fail(PCM_E_HIP, "reloc sort setup");
+            break;
+        }
+        if ((err = rocprim::radix_sort_pairs_desc(tmp, tb, k1, k2, v1, v2, (size_t)n, 0u, 64u, s))) {
+            rc = fail(PCM_E_HIP, "reloc sort");
+            break;
+        }
+        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+            using TT = decltype(T);
+            constexpr int D = decltype(DD)::value;
+            k_reloc_gather<TT, D><<<blocks_for(m), 256, 0, s>>>(k2, v2, m, n, (const TT *)e->xs, e->npad, e->lab, e->qe,
+                                                               (RelocRec *)records);
+            LAUNCHCHK();
+            return 0;
+        });
+        if (rc) break;
+        if ((err = hipStreamSynchronize(s))) { rc = fail(PCM_E_HIP, "reloc sync"); break; }
+    } while (0);
+    void *ps[] = {k1, k2, v1, v2, tmp};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    return rc;
+}
+
+int pcm_reloc_apply(pcm_engine *e, const void *records, int n_rec, void *stream) {
+    if (!e || !records || n_rec < 1) return fail(PCM_E_ARG, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    if (n_rec > e->rank_cap) {
+        if (e->rank_buf) HIPCHK(hipFree(e->rank_buf));
+        e->rank_buf = nullptr;
+        HIPCHK(hipMalloc(&e->rank_buf, (size_t)n_rec * sizeof(int)));
+        e->rank_cap = n_rec;
+    }
+    int rc = dispatch_d(e->d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_reloc_apply<D><<<1, 256, 0, s>>>((const RelocRec *)records, n_rec, e->held, e->k, e->rank_buf, e->ctrl);
+        LAUNCHCHK();
+        return 0;
+    });
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(e->stats, e->held, ((size_t)e->k * (e->d + 1) + 1) * sizeof(unsigned long long),
+                          hipMemcpyDeviceToDevice, s));
+    return pcm_iter_global(e, stream);
+}
+
+int pcm_final(pcm_engine *e, void *stream) {
+    if (!e) return fail(PCM_E_ARG, "null engine");
+    if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(&e->ctrl->inertia, 0, sizeof(double), s));
+    if (int rc = launch_candidates(e, s, 0)) return rc;
+    AssignArgs A = assign_args(e);
+    return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        if (e->ntiles > 0) {
+            k_assign<TT, D, 1><<<assign_grid(e), TPB, 0, s>>>(A);
+            LAUNCHCHK();
+        }
+        return 0;
+    });
+}
+
+int pcm_labels(pcm_engine *e, int32_t *out, void *stream) {
+    if (!e || (!out && e->n > 0)) return fail(PCM_E_ARG, "bad argument");
+    if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
+    if (e->n == 0) return 0;
+    k_unpermute<<<blocks_for(e->n), 256, 0, (hipStream_t)stream>>>(e->lab, e->perm, e->n, out);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pcm_get_centers(pcm_engine *e, float *out, void *stream) {
+    if (!e || !out) return fail(PCM_E_ARG, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    return dispatch_d(e->d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_centers_out<D><<<blocks_for(e->k), 256, 0, s>>>(e->C, e->k, out);
+        LAUNCHCHK();
+        return 0;
+    });
+}
+
+int pcm_history(pcm_engine *e, uint64_t *changed, double *shift, int cap, void *stream) {
+    if (!e || !changed || !shift || cap < 0) return fail(PCM_E_ARG, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    int c = std::min(cap, e->max_iter_cap);
+    HIPCHK(hipMemcpyAsync(changed, e->hist_changed, (size_t)c * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(shift, e->hist_shift, (size_t)c * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream) {
+    if (!e || !out) return fail(PCM_E_ARG, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    Ctrl h{};
+    HIPCHK(hipMemcpyAsync(&h, e->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    out->halt = h.halt;
+    out->done = h.done;
+    out->iter = h.iter;
+    out->n_empty = h.n_empty;
+    out->inertia = h.inertia;
+    out->last_changed = h.last_changed;
+    out->last_shift = h.last_shift;
+    return 0;
+}
+
+int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid) {
+    if (!e || !ncells || !ntiles || !grid) return fail(PCM_E_ARG, "bad argument");
+    *ncells = e->g.ncells;
+    *ntiles = e->ntiles;
+    for (int a = 0; a < MAXD; ++a) grid[a] = e->g.G[a];
+    return 0;
+}
+
+int pcm_candidate_stats(pcm_engine *e, double *mean, int *mx, int64_t *full_cells, void *stream) {
+    if (!e || !mean || !mx || !full_cells) return fail(PCM_E_ARG, "bad argument");
+    if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(e->cand_stats, 0, 3 * sizeof(unsigned long long), s));
+    k_cand_stats<<<blocks_for(e->g.ncells), 256, 0, s>>>(e->fc_cnt, e->g.ncells, e->cand_stats);
+    LAUNCHCHK();
+    unsigned long long h[3];
+    HIPCHK(hipMemcpyAsync(h, e->cand_stats, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    long long nonfull = e->g.ncells - (long long)h[2];
+    *mean = nonfull > 0 ? (double)h[0] / (double)nonfull : 0.0;
+    *mx = (int)h[1];
+    *full_cells = (int64_t)h[2];
+    return 0;
+}
+
+int pcm_synth_uniform(float *out, int64_t n, int d, uint64_t seed, int64_t start, void *stream) {
+    if ((!out && n > 0) || n < 0 || d < 1) return fail(PCM_E_ARG, "bad argument");
+    if (n == 0) return 0;
+    k_synth<<<blocks_for(n * d), 256, 0, (hipStream_t)stream>>>(out, n, d, seed, start);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pcm_synth_rows(float *out, const int64_t *rows, int64_t m, int d, uint64_t seed, void *stream) {
+    if ((!out || !rows) && m > 0) return fail(PCM_E_ARG, "bad argument");
+    if (m == 0) return 0;
+    k_synth_rows<<<blocks_for(m * d), 256, 0, (hipStream_t)stream>>>(out, (const long long *)rows, m, d, seed);
+    LAUNCHCHK();
+    return 0;
+}
+
+int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int k, const int32_t *q, int32_t *labels,
+                          uint64_t *stats, void *stream) {
+    if ((!X && n > 0) || !C || !q || (!labels && n > 0) || k < 1 || n < 0) return fail(PCM_E_ARG, "bad argument");
+    if ((size_t)k * sizeof(float4) > 160 * 1024) return fail(PCM_E_ARG, "k too large for LDS staging");
+    if (n == 0) return 0;
+    QExp qe{};
+    for (int a = 0; a < MAXD; ++a) qe.q[a] = a < d ? q[a] : 0;
+    hipStream_t s = (hipStream_t)stream;
+    int nblk = (int)std::min<long long>((n + 255) / 256, 2048);
+    return dispatch_d(d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_bruteforce<D><<<nblk, 256, (size_t)k * sizeof(float4), s>>>(X, n, C, k, qe, labels,
+                                                                       (unsigned long long *)stats);
+        LAUNCHCHK();
+        return 0;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,966 @@
+// pcm_kernels.hpp — gfx950 kernels of the multi-day point-cloud Lloyd engine.
+//
+// Hot path: per iteration
+//   k_coarse / k_fine  exact candidate lists per grid cell (fp64 bisector bound)
+//   k_assign           nearest centroid over the cell's candidates + LDS-privatised
+//                      fixed-point accumulation (replaces _k_means_lloyd.pyx:168-218)
+//   k_fold             replica fold of the partials (replaces the locked reduction
+//                      of _k_means_lloyd.pyx:142-152)
+//   k_global           averaging / shift / convergence (_k_means_common.pyx:274-311,
+//                      _kmeans.py:717-732)
+// Layout (once per cloud): k_bbox*, k_cellid, rocprim radix sort, k_gather,
+// k_cell_starts, k_tiles.
+//
+// Canonical arithmetic (oracle/lloyd_ref.py): fp32 distance
+// ((d0*d0 + d1*d1) + d2*d2) + d3*d3 with every op rounded (-ffp-contract=off),
+// strict '<' scan in ascending centroid index, int64 fixed-point sums.
+#pragma once
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pcm {
+
+constexpr int MAXD = 4;
+constexpr int CAPC = 256;          // coarse candidate capacity
+constexpr int CAPF = 64;           // fine candidate capacity
+constexpr int MSLOT = 8;           // LDS-privatised slots per lane
+constexpr int TPB = 256;           // assign block size
+constexpr int TILE = 8192;         // max points per tile (<= 63 per lane per flush)
+constexpr int NREP = 8;            // replicas of the global partials
+constexpr uint32_t FULL = 0xFFFFFFFFu;
+constexpr int QBITS = 25;
+constexpr uint32_t OFFS = 1u << QBITS;
+// Pruning margins (see DESIGN.md "Exactness of pruning").
+constexpr double PEPS = 7.62939453125e-06;   // 2^-17  >> 6 * 2^-24 (fp32 distance error)
+constexpr double PTAU = 1e-36;               // >> fp32 underflow error of a distance
+
+struct Grid {
+    int d;
+    int prune;
+    int F;
+    int pad_;
+    int G[MAXD];
+    int GC[MAXD];
+    double lo[MAXD], w[MAXD], inv[MAXD], mg[MAXD], ext[MAXD];
+    long long ncells, ncoarse;
+};
+
+// Device control block (one per engine).
+struct Ctrl {
+    uint32_t halt, done, iter, max_iter;
+    uint32_t n_empty, resume, status, pad0;
+    double tol;
+    double inertia;
+    unsigned long long changed_local;
+    unsigned long long last_changed;
+    double last_shift;
+};
+
+// Fixed-point exponents q_a (identical on every rank).
+struct QExp {
+    int q[MAXD];
+};
+
+// Control words are written by earlier kernels on the same stream; the kernel
+// boundary orders them, so plain loads suffice.
+__device__ __forceinline__ bool gated(const Ctrl *c) { return (c->halt | c->done) != 0u; }
+
+// ------------------------------------------------------------------ helpers
+template <int D>
+__device__ __forceinline__ float dist_canon(const float (&x)[D], const float4 &c) {
+    float a = x[0] - c.x;
+    float acc = a * a;
+    if (D > 1) { float b = x[1] - c.y; float s = b * b; acc = acc + s; }
+    if (D > 2) { float b = x[2] - c.z; float s = b * b; acc = acc + s; }
+    if (D > 3) { float b = x[3] - c.w; float s = b * b; acc = acc + s; }
+    return acc;
+}
+
+__device__ __forceinline__ float comp(const float4 &c, int a) {
+    return a == 0 ? c.x : a == 1 ? c.y : a == 2 ? c.z : c.w;
+}
+
+__device__ __forceinline__ uint32_t fixed_u(float x, int q) {
+    return (uint32_t)((int)__builtin_rintf(__builtin_ldexpf(x, q)) + (int)OFFS);
+}
+
+__device__ __forceinline__ void decode(long long c, const int *G, int d, int *idx) {
+    for (int a = d - 1; a >= 0; --a) {
+        idx[a] = (int)(c % G[a]);
+        c /= G[a];
+    }
+}
+
+__device__ __forceinline__ long long encode(const int *idx, const int *G, int d) {
+    long long c = 0;
+    for (int a = 0; a < d; ++a) c = c * G[a] + idx[a];
+    return c;
+}
+
+// fine-cell range [f0, f1] on every axis -> fp64 box containing every point binned there
+__device__ __forceinline__ void cell_box(const Grid &g, const int *f0, const int *f1, double *blo, double *bhi) {
+    for (int a = 0; a < g.d; ++a) {
+        blo[a] = g.lo[a] + (double)f0[a] * g.w[a] - g.mg[a];
+        bhi[a] = (f1[a] == g.G[a] - 1) ? g.lo[a] + g.ext[a] + g.mg[a]
+                                       : g.lo[a] + (double)(f1[a] + 1) * g.w[a] + g.mg[a];
+    }
+}
+
+template <int D>
+__device__ __forceinline__ double maxdist(const double *blo, const double *bhi, const float4 &c) {
+    double s = 0.0;
+    for (int a = 0; a < D; ++a) {
+        double ca = (double)comp(c, a);
+        double l = blo[a] - ca, h = bhi[a] - ca;
+        s += fmax(l * l, h * h);
+    }
+    return s;
+}
+
+// True iff every point of the box is provably (with margin PEPS/PTAU) strictly
+// closer, in the canonical fp32 distance, to r than to c.  The objective
+// (1-e)|x-c|^2 - (1+e)|x-r|^2 is separable and concave per axis, so its box
+// minimum is the sum of per-axis endpoint minima.
+template <int D>
+__device__ __forceinline__ bool prunable(const double *blo, const double *bhi, const float4 &c, const float4 &r) {
+    const double em = 1.0 - PEPS, ep = 1.0 + PEPS;
+    double s = 0.0;
+    for (int a = 0; a < D; ++a) {
+        double ca = (double)comp(c, a), ra = (double)comp(r, a);
+        double cl = blo[a] - ca, ch = bhi[a] - ca, rl = blo[a] - ra, rh = bhi[a] - ra;
+        double gl = em * (cl * cl) - ep * (rl * rl);
+        double gh = em * (ch * ch) - ep * (rh * rh);
+        s += fmin(gl, gh);
+    }
+    return s > PTAU;
+}
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<__half>(__half v) { return __half2float(v); }
+
+// ------------------------------------------------------------------ layout
+// Per-block min/max/maxabs (+ non-finite flag) of an AoS (n, D) array.
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_bbox_partial(const T *__restrict__ X, long long n, float *__restrict__ part,
+                                                      unsigned *__restrict__ nonfinite) {
+    float mn[D], mx[D];
+    for (int a = 0; a < D; ++a) { mn[a] = __builtin_inff(); mx[a] = -__builtin_inff(); }
+    bool bad = false;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        for (int a = 0; a < D; ++a) {
+            float v = to_f<T>(X[i * D + a]);
+            bad |= !__builtin_isfinite(v);
+            mn[a] = fminf(mn[a], v);
+            mx[a] = fmaxf(mx[a], v);
+        }
+    }
+    __shared__ float smn[D][256], smx[D][256];
+    for (int a = 0; a < D; ++a) { smn[a][threadIdx.x] = mn[a]; smx[a][threadIdx.x] = mx[a]; }
+    if (bad) atomicOr(nonfinite, 1u);
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s)
+            for (int a = 0; a < D; ++a) {
+                smn[a][threadIdx.x] = fminf(smn[a][threadIdx.x], smn[a][threadIdx.x + s]);
+                smx[a][threadIdx.x] = fmaxf(smx[a][threadIdx.x], smx[a][threadIdx.x + s]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int a = 0; a < D; ++a) {
+            part[(size_t)blockIdx.x * 2 * D + a] = smn[a][0];
+            part[(size_t)blockIdx.x * 2 * D + D + a] = smx[a][0];
+        }
+}
+
+template <int D>
+__global__ void k_bbox_final(const float *__restrict__ part, int nblk, double *__restrict__ out) {
+    // out: lo[D], hi[D]
+    if (threadIdx.x != 0) return;
+    for (int a = 0; a < D; ++a) {
+        float mn = __builtin_inff(), mx = -__builtin_inff();
+        for (int b = 0; b < nblk; ++b) {
+            mn = fminf(mn, part[(size_t)b * 2 * D + a]);
+            mx = fmaxf(mx, part[(size_t)b * 2 * D + D + a]);
+        }
+        out[a] = mn;
+        out[D + a] = mx;
+    }
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long long n, Grid g, uint32_t *__restrict__ keys,
+                                                uint32_t *__restrict__ vals) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int idx[MAXD];
+    for (int a = 0; a < D; ++a) {
+        double t = ((double)to_f<T>(X[i * D + a]) - g.lo[a]) * g.inv[a];
+        int v = (int)floor(t);
+        v = v < 0 ? 0 : (v >= g.G[a] ? g.G[a] - 1 : v);
+        idx[a] = v;
+    }
+    keys[i] = (uint32_t)encode(idx, g.G, D);
+    vals[i] = (uint32_t)i;
+}
+
+// SoA gather into cell order; labels := -1
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long long n, long long npad,
+                                                const uint32_t *__restrict__ perm, T *__restrict__ xs,
+                                                int32_t *__restrict__ lab) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= npad) return;
+    if (i < n) {
+        long long s = perm[i];
+        for (int a = 0; a < D; ++a) xs[a * npad + i] = X[s * D + a];
+    } else {
+        for (int a = 0; a < D; ++a) xs[a * npad + i] = (T)0.0f;
+    }
+    lab[i] = -1;
+}
+
+// cell_start[c] = first sorted index with key >= c, for c in [0, ncells]
+__global__ __launch_bounds__(256) void k_cell_starts(const uint32_t *__restrict__ keys, long long n, long long ncells,
+                                                     uint32_t *__restrict__ start) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i > n) return;
+    long long prev = (i == 0) ? -1 : (long long)keys[i - 1];
+    long long cur = (i == n) ? ncells : (long long)keys[i];
+    for (long long c = prev + 1; c <= cur; ++c) start[c] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(256) void k_tile_counts(const uint32_t *__restrict__ start, long long ncells,
+                                                     uint32_t *__restrict__ cnt) {
+    long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    uint32_t n = start[c + 1] - start[c];
+    cnt[c] = (n + TILE - 1) / TILE;
+}
+
+__global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__ start, const uint32_t *__restrict__ off,
+                                                    long long ncells, uint4 *__restrict__ tiles) {
+    long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    uint32_t s = start[c], e = start[c + 1];
+    uint32_t n = e - s;
+    if (n == 0) return;
+    uint32_t nt = (n + TILE - 1) / TILE;
+    uint32_t per = (n + nt - 1) / nt;
+    uint32_t o = off[c];
+    for (uint32_t t = 0; t < nt; ++t) {
+        uint32_t a = s + t * per;
+        uint32_t b = a + per < e ? a + per : e;
+        tiles[o + t] = make_uint4((uint32_t)c, a, b, 0u);
+    }
+}
+
+// ------------------------------------------------------------------ candidates
+// One block per coarse cell: reference r = argmin_c maxdist(c, box), keep every
+// centroid not provably dominated by r.  List ascending in centroid index.
+template <int D>
+__global__ __launch_bounds__(256) void k_coarse(Grid g, const float4 *__restrict__ C, int K,
+                                                uint32_t *__restrict__ cc_cnt, uint32_t *__restrict__ cc_idx,
+                                                const Ctrl *__restrict__ ctrl, int gate) {
+    if (gate && gated(ctrl)) return;
+    const long long I = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (!g.prune) {
+        if (tid == 0) cc_cnt[I] = FULL;
+        return;
+    }
+    int ci[MAXD], f0[MAXD], f1[MAXD];
+    decode(I, g.GC, D, ci);
+    for (int a = 0; a < D; ++a) {
+        f0[a] = ci[a] * g.F;
+        f1[a] = min(f0[a] + g.F, g.G[a]) - 1;
+    }
+    double blo[MAXD], bhi[MAXD];
+    cell_box(g, f0, f1, blo, bhi);
+
+    double best = __builtin_inf();
+    int bj = 0x7fffffff;
+    for (int j = tid; j < K; j += 256) {
+        double m = maxdist<D>(blo, bhi, C[j]);
+        if (m < best) { best = m; bj = j; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        double ob = __shfl_xor(best, o);
+        int oj = __shfl_xor(bj, o);
+        if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+    }
+    __shared__ double sb[4];
+    __shared__ int sj[4];
+    __shared__ uint32_t wcnt[4];
+    if (lane == 0) { sb[wv] = best; sj[wv] = bj; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 4; ++w)
+            if (sb[w] < sb[0] || (sb[w] == sb[0] && sj[w] < sj[0])) { sb[0] = sb[w]; sj[0] = sj[w]; }
+    }
+    __syncthreads();
+    const float4 r = C[sj[0]];
+    uint32_t total = 0;
+    for (int base = 0; base < K; base += 256) {
+        int j = base + tid;
+        bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r);
+        unsigned long long bal = __ballot(keep);
+        uint32_t pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wcnt[wv] = __popcll(bal);
+        __syncthreads();
+        uint32_t woff = 0;
+        for (int w = 0; w < wv; ++w) woff += wcnt[w];
+        uint32_t pos = total + woff + pre;
+        if (keep && pos < (uint32_t)CAPC) cc_idx[I * CAPC + pos] = (uint32_t)j;
+        total += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        __syncthreads();
+    }
+    if (tid == 0) cc_cnt[I] = total <= (uint32_t)CAPC ? total : FULL;
+}
+
+// A cell's candidate count goes to fc_cnt and into the .w of each of its tiles
+// (so the assign kernel reaches its candidates in one dependent load).
+__device__ __forceinline__ void publish_m(long long cell, uint32_t m, uint32_t *fc_cnt, const uint32_t *toff,
+                                          uint4 *tiles) {
+    fc_cnt[cell] = m;
+    for (uint32_t o = toff[cell]; o < toff[cell + 1]; ++o) tiles[o].w = m;
+}
+
+// One block per coarse cell; each wave refines children using the parent list.
+template <int D>
+__global__ __launch_bounds__(256) void k_fine(Grid g, const float4 *__restrict__ C, int K,
+                                              const uint32_t *__restrict__ cc_cnt, const uint32_t *__restrict__ cc_idx,
+                                              uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
+                                              int32_t *__restrict__ fc_lab, const uint32_t *__restrict__ toff,
+                                              uint4 *__restrict__ tiles, const Ctrl *__restrict__ ctrl, int gate) {
+    if (gate && gated(ctrl)) return;
+    const long long I = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ float4 prec[CAPC];
+    __shared__ int pidx[CAPC];
+    int ci[MAXD];
+    decode(I, g.GC, D, ci);
+    uint32_t mp = cc_cnt[I];
+    const bool pfull = (mp == FULL);
+    if (pfull) mp = (uint32_t)K;
+    if (!pfull)
+        for (uint32_t l = tid; l < mp; l += 256) {
+            int j = (int)cc_idx[I * CAPC + l];
+            pidx[l] = j;
+            prec[l] = C[j];
+        }
+    __syncthreads();
+    int nch = 1;
+    for (int a = 0; a < D; ++a) nch *= g.F;
+    for (int ch = wv; ch < nch; ch += 4) {
+        int o[MAXD], f[MAXD];
+        int t = ch;
+        bool ok = true;
+        for (int a = D - 1; a >= 0; --a) {
+            o[a] = t % g.F;
+            t /= g.F;
+            f[a] = ci[a] * g.F + o[a];
+            ok &= f[a] < g.G[a];
+        }
+        if (!ok) continue;
+        const long long cell = encode(f, g.G, D);
+        if (!g.prune) {
+            if (lane == 0) publish_m(cell, FULL, fc_cnt, toff, tiles);
+            continue;
+        }
+        double blo[MAXD], bhi[MAXD];
+        cell_box(g, f, f, blo, bhi);
+        double best = __builtin_inf();
+        int bj = 0x7fffffff;
+        for (uint32_t l = lane; l < mp; l += 64) {
+            float4 c = pfull ? C[l] : prec[l];
+            int j = pfull ? (int)l : pidx[l];
+            double m = maxdist<D>(blo, bhi, c);
+            if (m < best) { best = m; bj = j; }
+        }
+        for (int s = 32; s > 0; s >>= 1) {
+            double ob = __shfl_xor(best, s);
+            int oj = __shfl_xor(bj, s);
+            if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+        }
+        const float4 r = C[bj];
+        uint32_t total = 0;
+        for (uint32_t base = 0; base < mp; base += 64) {
+            uint32_t l = base + lane;
+            bool in = l < mp;
+            float4 c = in ? (pfull ? C[l] : prec[l]) : r;
+            int j = in ? (pfull ? (int)l : pidx[l]) : 0;
+            bool keep = in && !prunable<D>(blo, bhi, c, r);
+            unsigned long long bal = __ballot(keep);
+            uint32_t pos = total + __popcll(bal & ((1ull << lane) - 1ull));
+            if (keep && pos < (uint32_t)CAPF) {
+                fc_rec[cell * CAPF + pos] = c;
+                fc_lab[cell * CAPF + pos] = j;
+            }
+            total += __popcll(bal);
+        }
+        if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, toff, tiles);
+    }
+}
+
+// ------------------------------------------------------------------ assign
+// Nearest of mm candidates for 4 points per lane: strict '<' in ascending
+// candidate order, so the lowest index wins ties (_k_means_lloyd.pyx:205-213).
+template <int D, typename P>
+__device__ __forceinline__ void scan4(P rec, int mm, const float (&x)[4][D], float (&bd)[4], int (&bj)[4]) {
+    {
+        const float4 c = rec[0];
+        for (int e = 0; e < 4; ++e) { bd[e] = dist_canon<D>(x[e], c); bj[e] = 0; }
+    }
+    for (int j = 1; j < mm; ++j) {
+        const float4 c = rec[j];
+        for (int e = 0; e < 4; ++e) {
+            float dd = dist_canon<D>(x[e], c);
+            bool lt = dd < bd[e];
+            bd[e] = lt ? dd : bd[e];
+            bj[e] = lt ? j : bj[e];
+        }
+    }
+}
+
+struct AssignArgs {
+    const void *xs;                 // SoA [D][npad] of T
+    long long npad;
+    const uint4 *tiles;             // {cell, start, end, m}; m written by k_fine each iteration
+    long long ntiles;
+    const float4 *fc_rec;
+    const int32_t *fc_lab;
+    const float4 *C;                // all centres (FULL cells)
+    int K;
+    int q[MAXD];
+    int32_t *lab;                   // sorted-order labels (in: previous, out: new)
+    unsigned long long *partials;   // [NREP][K][D+1]
+    Ctrl *ctrl;
+};
+
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+    static __device__ __forceinline__ void load(const float *p, float (&v)[4]) {
+        float4 t = *reinterpret_cast<const float4 *>(p);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    }
+};
+template <> struct Vec4<__half> {
+    static __device__ __forceinline__ void load(const __half *p, float (&v)[4]) {
+        uint2 t = *reinterpret_cast<const uint2 *>(p);
+        __half2 a = *reinterpret_cast<__half2 *>(&t.x), b = *reinterpret_cast<__half2 *>(&t.y);
+        v[0] = __low2float(a); v[1] = __high2float(a); v[2] = __low2float(b); v[3] = __high2float(b);
+    }
+};
+
+struct TileH {
+    long long cell, start, end, base0;
+    int mm, nr, full, pad_;
+};
+
+__device__ __forceinline__ TileH make_hdr(const uint4 &t, int K) {
+    TileH h;
+    h.cell = t.x;
+    h.start = t.y;
+    h.end = t.z;
+    h.full = (t.w == FULL) ? 1 : 0;
+    h.mm = h.full ? K : (int)t.w;
+    h.base0 = h.start & ~3LL;
+    h.nr = (int)((h.end - h.base0 + 4 * TPB - 1) / (4 * TPB));
+    return h;
+}
+
+// One lane's 4 consecutive points (SoA dwordx4 / fp16 dwordx2 per axis) + previous labels.
+template <int D>
+struct Pts {
+    float x[4][D];
+    int old[4];
+};
+
+template <typename T, int D>
+__device__ __forceinline__ void load_pts(const T *__restrict__ xs, long long npad, const int32_t *__restrict__ lab,
+                                         long long i0, long long end, Pts<D> &p) {
+    if (i0 < end) {
+        float v[4];
+        for (int a = 0; a < D; ++a) {
+            Vec4<T>::load(xs + a * npad + i0, v);
+            for (int e = 0; e < 4; ++e) p.x[e][a] = v[e];
+        }
+        const int4 o = *reinterpret_cast<const int4 *>(lab + i0);
+        p.old[0] = o.x; p.old[1] = o.y; p.old[2] = o.z; p.old[3] = o.w;
+    } else {
+        for (int e = 0; e < 4; ++e) {
+            for (int a = 0; a < D; ++a) p.x[e][a] = 0.f;
+            p.old[e] = 0;
+        }
+    }
+}
+
+// Persistent, software-pipelined assignment.  Each block walks tiles
+// blockIdx.x, +gridDim.x, ...; while it computes one round of 1024 points it
+// already has the next round (or the next tile's first round, candidate record
+// and header) in flight.  Per tile: candidates -> LDS, rounds of 4 points per
+// lane, then the LDS-privatised per-lane slot sums are folded (8 threads per
+// (slot, quantity) pair) into the global int64 partials and re-zeroed.
+// MODE 0: Lloyd iteration (labels, change count, statistics); gated.
+// MODE 1: final E-step (labels + inertia); not gated by `done`.
+template <typename T, int D, int MODE>
+__global__ __launch_bounds__(TPB) void k_assign(AssignArgs A) {
+    if (MODE == 0 && gated(A.ctrl)) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [MSLOT][D+1][TPB]
+    __shared__ float4 srec[CAPF];
+    __shared__ int32_t slab[CAPF];
+    const int tid = threadIdx.x;
+    long long t = blockIdx.x;
+    if (t >= A.ntiles) return;
+    const T *__restrict__ xs = reinterpret_cast<const T *>(A.xs);
+
+    if (MODE == 0)
+        for (int e = tid; e < MSLOT * (D + 1) * TPB / 4; e += TPB)
+            reinterpret_cast<uint4 *>(acc)[e] = make_uint4(0u, 0u, 0u, 0u);
+
+    // prologue: first tile's header, candidate record and first round
+    TileH h = make_hdr(A.tiles[t], A.K);
+    float4 crec = make_float4(0.f, 0.f, 0.f, 0.f);
+    int clab = 0;
+    if (!h.full && tid < h.mm) {
+        crec = A.fc_rec[h.cell * CAPF + tid];
+        clab = A.fc_lab[h.cell * CAPF + tid];
+    }
+    Pts<D> cur;
+    load_pts<T, D>(xs, A.npad, A.lab, h.base0 + 4 * tid, h.end, cur);
+
+    uint32_t nch = 0;
+    double inert = 0.0;
+    unsigned long long *prep = A.partials + (size_t)(blockIdx.x % NREP) * A.K * (D + 1);
+    while (true) {
+        __syncthreads();   // previous tile's readers of srec/slab/acc are done
+        if (!h.full && tid < h.mm) {
+            srec[tid] = crec;
+            slab[tid] = clab;
+        }
+        __syncthreads();
+        const long long tn = t + gridDim.x;
+        const bool has_next = tn < A.ntiles;
+        uint4 tln = make_uint4(0u, 0u, 0u, 0u);
+        if (has_next) tln = A.tiles[tn];
+        TileH hn = h;
+        for (int r = 0; r < h.nr; ++r) {
+            const long long i0 = h.base0 + (long long)r * 4 * TPB + 4 * tid;
+            Pts<D> nxt;
+            if (r + 1 < h.nr) {
+                load_pts<T, D>(xs, A.npad, A.lab, i0 + 4 * TPB, h.end, nxt);
+            } else if (has_next) {
+                hn = make_hdr(tln, A.K);
+                load_pts<T, D>(xs, A.npad, A.lab, hn.base0 + 4 * tid, hn.end, nxt);
+                if (!hn.full && tid < hn.mm) {
+                    crec = A.fc_rec[hn.cell * CAPF + tid];
+                    clab = A.fc_lab[hn.cell * CAPF + tid];
+                }
+            }
+            if (i0 < h.end) {
+                bool v[4];
+                for (int e = 0; e < 4; ++e) v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
+                float bd[4];
+                int bj[4];
+                if (h.full)
+                    scan4<D>(A.C, h.mm, cur.x, bd, bj);
+                else
+                    scan4<D>(srec, h.mm, cur.x, bd, bj);
+                int lb[4];
+                for (int e = 0; e < 4; ++e) lb[e] = h.full ? bj[e] : slab[bj[e]];
+                if (v[0] & v[1] & v[2] & v[3]) {
+                    *reinterpret_cast<int4 *>(A.lab + i0) = make_int4(lb[0], lb[1], lb[2], lb[3]);
+                } else {
+                    for (int e = 0; e < 4; ++e)
+                        if (v[e]) A.lab[i0 + e] = lb[e];
+                }
+                if (MODE == 0) {
+                    for (int e = 0; e < 4; ++e) {
+                        if (!v[e]) continue;
+                        nch += (lb[e] != cur.old[e]) ? 1u : 0u;
+#ifdef PCM_ABL_NOACC
+                        continue;
+#endif
+                        const int s = bj[e];
+                        if (s < MSLOT) {
+                            for (int a = 0; a < D; ++a)
+                                atomicAdd(&acc[(s * (D + 1) + a) * TPB + tid], fixed_u(cur.x[e][a], A.q[a]));
+                            atomicAdd(&acc[(s * (D + 1) + D) * TPB + tid], 1u);
+                        } else {
+                            unsigned long long *p = prep + (size_t)lb[e] * (D + 1);
+                            for (int a = 0; a < D; ++a)
+                                atomicAdd(p + a, (unsigned long long)fixed_u(cur.x[e][a], A.q[a]));
+                            atomicAdd(p + D, 1ull);
+                        }
+                    }
+                } else {
+                    for (int e = 0; e < 4; ++e)
+                        if (v[e]) inert += (double)bd[e];
+                }
+            }
+            cur = nxt;
+        }
+        if (MODE == 0) {
+            __syncthreads();   // every lane's slot sums of this tile are in LDS
+#ifdef PCM_ABL_NOFLUSH
+            const int nslots = 0;
+#else
+            const int nslots = h.mm < MSLOT ? h.mm : MSLOT;
+#endif
+            const int npairs = nslots * (D + 1);
+            for (int p0 = 0; p0 < npairs; p0 += TPB / 8) {
+                const int p = p0 + tid / 8, sub = tid & 7;
+                unsigned long long s = 0;
+                if (p < npairs)
+                    for (int k = 0; k < TPB / 8; ++k) {
+                        uint32_t *a = &acc[p * TPB + sub + 8 * k];
+                        s += *a;
+                        *a = 0u;   // re-zero for the next tile (same thread, no race)
+                    }
+                s += __shfl_down(s, 4, 8);
+                s += __shfl_down(s, 2, 8);
+                s += __shfl_down(s, 1, 8);
+                if (p < npairs && sub == 0 && s) {
+                    const int slot = p / (D + 1), qq = p % (D + 1);
+                    const int lbl = h.full ? slot : slab[slot];
+                    atomicAdd(prep + (size_t)lbl * (D + 1) + qq, s);
+                }
+            }
+        }
+        if (!has_next) break;
+        t = tn;
+        h = hn;
+    }
+
+    if (MODE == 0) {
+        for (int o = 32; o > 0; o >>= 1) nch += __shfl_xor(nch, o);
+        if ((tid & 63) == 0 && nch) atomicAdd(&A.ctrl->changed_local, (unsigned long long)nch);
+    } else {
+        for (int o = 32; o > 0; o >>= 1) inert += __shfl_xor(inert, o);
+        if ((tid & 63) == 0) atomicAdd(&A.ctrl->inertia, inert);
+    }
+}
+
+// stats[j*(D+1)+q] = sum over replicas; partials := 0; stats[K*(D+1)] = changes
+template <int D>
+__global__ __launch_bounds__(256) void k_fold(unsigned long long *__restrict__ partials, int K,
+                                              unsigned long long *__restrict__ stats, Ctrl *__restrict__ ctrl) {
+    if (gated(ctrl)) return;
+    const int n = K * (D + 1);
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        unsigned long long s = 0;
+        for (int r = 0; r < NREP; ++r) {
+            s += partials[(size_t)r * n + i];
+            partials[(size_t)r * n + i] = 0ull;
+        }
+        stats[i] = s;
+    }
+    if (i == n) {
+        stats[n] = ctrl->changed_local;
+        ctrl->changed_local = 0ull;
+    }
+}
+
+// Single block of 1024 threads.  Reads the (all-reduced) statistics, halts for
+// relocation when a cluster is empty (unless resuming), otherwise averages,
+// computes the shift with the fixed reduction tree and sets convergence flags.
+template <int D>
+__global__ __launch_bounds__(1024) void k_global(const unsigned long long *__restrict__ stats, int K, QExp qe,
+                                                 unsigned long long *__restrict__ held,
+                                                 float4 *__restrict__ C, float4 *__restrict__ Cn,
+                                                 unsigned long long *__restrict__ hist_changed,
+                                                 double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl) {
+    if (gated(ctrl)) return;
+    const int tid = threadIdx.x;
+    const int *q = qe.q;
+    __shared__ unsigned cnt_empty;
+    __shared__ unsigned long long smax[1024];
+    __shared__ int sarg[1024];
+    __shared__ double ssum[1024];
+    if (tid == 0) cnt_empty = 0;
+    __syncthreads();
+    unsigned long long bmax = 0;
+    int barg = 0x7fffffff;
+    unsigned ne = 0;
+    for (int j = tid; j < K; j += 1024) {
+        unsigned long long c = stats[(size_t)j * (D + 1) + D];
+        if (c == 0) ne++;
+        if (c > bmax) { bmax = c; barg = j; }
+    }
+    atomicAdd(&cnt_empty, ne);
+    smax[tid] = bmax;
+    sarg[tid] = barg;
+    __syncthreads();
+    const uint32_t resume = ctrl->resume;
+    if (cnt_empty > 0 && !resume) {
+        // Snapshot the reduced statistics: the no-op iterations queued behind a
+        // halt still run their all-reduce on `stats`.
+        for (int i = tid; i < K * (D + 1) + 1; i += 1024) held[i] = stats[i];
+        if (tid == 0) {
+            ctrl->halt = 1u;
+            ctrl->n_empty = cnt_empty;
+        }
+        return;
+    }
+    for (int s = 512; s > 0; s >>= 1) {
+        if (tid < s) {
+            unsigned long long o = smax[tid + s];
+            int oa = sarg[tid + s];
+            if (o > smax[tid] || (o == smax[tid] && oa < sarg[tid])) { smax[tid] = o; sarg[tid] = oa; }
+        }
+        __syncthreads();
+    }
+    const int argmax = sarg[0];
+    // average
+    for (int j = tid; j < K; j += 1024) {
+        const unsigned long long c = stats[(size_t)j * (D + 1) + D];
+        float out[4] = {0.f, 0.f, 0.f, 0.f};
+        if (c > 0) {
+            for (int a = 0; a < D; ++a) {
+                const long long sraw = (long long)stats[(size_t)j * (D + 1) + a];
+                const long long sv = sraw - (long long)c * (long long)OFFS;
+                const double m = ((double)sv * __builtin_ldexp(1.0, -q[a])) / (double)c;
+                out[a] = (float)m;
+            }
+            Cn[j] = make_float4(out[0], out[1], out[2], out[3]);
+        }
+    }
+    __syncthreads();
+    for (int j = tid; j < K; j += 1024) {
+        const unsigned long long c = stats[(size_t)j * (D + 1) + D];
+        if (c == 0) Cn[j] = (smax[0] > 0) ? Cn[argmax] : C[j];
+    }
+    __syncthreads();
+    // shift: per-thread sequential over j = tid + 1024 r, then halving tree
+    double acc = 0.0;
+    for (int j = tid; j < K; j += 1024) {
+        const float4 a4 = Cn[j], b4 = C[j];
+        double s = 0.0;
+        for (int a = 0; a < D; ++a) {
+            double dd = (double)comp(a4, a) - (double)comp(b4, a);
+            double sq = dd * dd;
+            s = (a == 0) ? sq : s + sq;
+        }
+        acc = acc + s;
+    }
+    ssum[tid] = acc;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if (tid < s) ssum[tid] = ssum[tid] + ssum[tid + s];
+        __syncthreads();
+    }
+    for (int j = tid; j < K; j += 1024) C[j] = Cn[j];
+    if (tid == 0) {
+        const unsigned long long changed = stats[(size_t)K * (D + 1)];
+        const double shift = ssum[0];
+        const uint32_t it = ctrl->iter;
+        if (it < ctrl->max_iter) {
+            hist_changed[it] = changed;
+            hist_shift[it] = shift;
+        }
+        ctrl->last_changed = changed;
+        ctrl->last_shift = shift;
+        ctrl->resume = 0u;
+        uint32_t done = 0;
+        if (changed == 0ull) done = 1u;
+        else if (shift <= ctrl->tol) done = 2u;
+        ctrl->iter = it + 1;
+        if (!done && it + 1 >= ctrl->max_iter) done = 3u;
+        ctrl->done = done;
+    }
+}
+
+// ------------------------------------------------------------------ relocation
+// key = dist_bits << 32 | (0xffffffff - global index); sort descending.
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_reloc_keys(const T *__restrict__ xs, long long n, long long npad,
+                                                    const int32_t *__restrict__ lab, const uint32_t *__restrict__ perm,
+                                                    const float4 *__restrict__ C, long long gidx0,
+                                                    unsigned long long *__restrict__ keys, uint32_t *__restrict__ vals) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float x[D];
+    for (int a = 0; a < D; ++a) x[a] = to_f<T>(xs[a * npad + i]);
+    float d = dist_canon<D>(x, C[lab[i]]);
+    unsigned long long g = (unsigned long long)(gidx0 + perm[i]);
+    keys[i] = ((unsigned long long)__float_as_uint(d) << 32) | (0xffffffffull - (g & 0xffffffffull));
+    vals[i] = (uint32_t)i;
+}
+
+struct RelocRec {
+    unsigned long long key;
+    int32_t label;
+    int32_t valid;
+    int32_t xq[4];
+};
+
+template <typename T, int D>
+__global__ void k_reloc_gather(const unsigned long long *__restrict__ keys, const uint32_t *__restrict__ vals, int m,
+                               long long n, const T *__restrict__ xs, long long npad, const int32_t *__restrict__ lab,
+                               QExp qe, RelocRec *__restrict__ out) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    RelocRec r;
+    r.key = 0ull; r.label = 0; r.valid = 0;
+    r.xq[0] = r.xq[1] = r.xq[2] = r.xq[3] = 0;
+    if (t < n) {
+        uint32_t i = vals[t];
+        r.key = keys[t];
+        r.label = lab[i];
+        r.valid = 1;
+        for (int a = 0; a < D; ++a) r.xq[a] = (int)fixed_u(to_f<T>(xs[a * npad + i]), qe.q[a]) - (int)OFFS;
+    }
+    out[t] = r;
+}
+
+// Single block: global top-n_empty over all ranks' records, moves applied to
+// the (all-reduced, offset-encoded) statistics in cluster order; then resume.
+template <int D>
+__global__ __launch_bounds__(256) void k_reloc_apply(const RelocRec *__restrict__ recs, int nrec,
+                                                     unsigned long long *__restrict__ stats, int K,
+                                                     int *__restrict__ rank_buf, Ctrl *__restrict__ ctrl) {
+    const int tid = threadIdx.x;
+    // rank of each valid record by (key desc); keys are globally unique
+    for (int i = tid; i < nrec; i += 256) {
+        int r = 0;
+        if (recs[i].valid) {
+            for (int j = 0; j < nrec; ++j)
+                if (recs[j].valid && recs[j].key > recs[i].key) ++r;
+        } else {
+            r = 0x7fffffff;
+        }
+        rank_buf[i] = r;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        // max distance == 0 -> nothing to relocate (sklearn _k_means_common.pyx:189-192)
+        int top = -1;
+        for (int i = 0; i < nrec; ++i)
+            if (rank_buf[i] == 0) top = i;
+        bool doit = top >= 0 && (recs[top].key >> 32) != 0ull;
+        if (doit) {
+            int done_moves = 0;
+            for (int j = 0; j < K; ++j) {
+                if (stats[(size_t)j * (D + 1) + D] != 0ull) continue;
+                int pick = -1;
+                for (int i = 0; i < nrec; ++i)
+                    if (rank_buf[i] == done_moves) { pick = i; break; }
+                if (pick < 0) break;
+                const RelocRec &r = recs[pick];
+                unsigned long long *so = stats + (size_t)r.label * (D + 1);
+                unsigned long long *sn = stats + (size_t)j * (D + 1);
+                for (int a = 0; a < D; ++a) {
+                    unsigned long long u = (unsigned long long)(long long)(r.xq[a] + (int)OFFS);
+                    so[a] -= u;
+                    sn[a] = u;
+                }
+                so[D] -= 1ull;
+                sn[D] = 1ull;
+                ++done_moves;
+            }
+        }
+        ctrl->halt = 0u;
+        ctrl->resume = 1u;
+    }
+}
+
+// ------------------------------------------------------------------ misc
+__global__ __launch_bounds__(256) void k_unpermute(const int32_t *__restrict__ lab, const uint32_t *__restrict__ perm,
+                                                   long long n, int32_t *__restrict__ out) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) out[perm[i]] = lab[i];
+}
+
+template <int D>
+__global__ void k_centers_in(const float *__restrict__ Cin, int K, float4 *__restrict__ C) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= K) return;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < D; ++a) v[a] = Cin[(size_t)j * D + a];
+    C[j] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <int D>
+__global__ void k_centers_out(const float4 *__restrict__ C, int K, float *__restrict__ out) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= K) return;
+    float4 c = C[j];
+    for (int a = 0; a < D; ++a) out[(size_t)j * D + a] = comp(c, a);
+}
+
+__global__ __launch_bounds__(256) void k_fill_i32(int32_t *__restrict__ p, long long n, int32_t v) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+__device__ __forceinline__ float synth_value(unsigned long long ctr, unsigned long long seed) {
+    unsigned long long z = seed * 0xD1B54A32D192ED03ull + (ctr + 1ull) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    return (float)(uint32_t)(z >> 40) * 5.9604644775390625e-08f;
+}
+
+__global__ __launch_bounds__(256) void k_synth(float *__restrict__ out, long long n, int d, unsigned long long seed,
+                                               long long start) {
+    long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (e >= n * d) return;
+    out[e] = synth_value((unsigned long long)(start * d + e), seed);
+}
+
+__global__ __launch_bounds__(256) void k_synth_rows(float *__restrict__ out, const long long *__restrict__ rows,
+                                                    long long m, int d, unsigned long long seed) {
+    long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (e >= m * d) return;
+    long long r = rows[e / d];
+    out[e] = synth_value((unsigned long long)(r * d + e % d), seed);
+}
+
+// Candidate-list statistics for diagnostics.
+__global__ __launch_bounds__(256) void k_cand_stats(const uint32_t *__restrict__ fc_cnt, long long ncells,
+                                                    unsigned long long *__restrict__ out /* sum, max, full */) {
+    long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    uint32_t m = fc_cnt[c];
+    if (m == FULL) { atomicAdd(out + 2, 1ull); return; }
+    atomicAdd(out, (unsigned long long)m);
+    atomicMax(out + 1, (unsigned long long)m);
+}
+
+// ------------------------------------------------------------------ brute force
+// Stateless brute-force operator: centres staged in LDS (K*4 floats), each
+// thread one point; statistics via global atomics (exactness over speed).
+template <int D>
+__global__ __launch_bounds__(256) void k_bruteforce(const float *__restrict__ X, long long n, const float *__restrict__ Cg,
+                                                    int K, QExp qe, int32_t *__restrict__ labels,
+                                                    unsigned long long *__restrict__ stats) {
+    extern __shared__ __attribute__((aligned(16))) float4 sc[];
+    for (int j = threadIdx.x; j < K; j += blockDim.x) {
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int a = 0; a < D; ++a) v[a] = Cg[(size_t)j * D + a];
+        sc[j] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    __syncthreads();
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        float x[D];
+        for (int a = 0; a < D; ++a) x[a] = X[i * D + a];
+        float bd = dist_canon<D>(x, sc[0]);
+        int bj = 0;
+        for (int j = 1; j < K; ++j) {
+            float dd = dist_canon<D>(x, sc[j]);
+            if (dd < bd) { bd = dd; bj = j; }
+        }
+        labels[i] = bj;
+        if (stats) {
+            unsigned long long *p = stats + (size_t)bj * (D + 1);
+            for (int a = 0; a < D; ++a) atomicAdd(p + a, (unsigned long long)fixed_u(x[a], qe.q[a]));
+            atomicAdd(p + D, 1ull);
+        }
+    }
+}
+
+}  // namespace pcm

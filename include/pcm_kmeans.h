@@ -1,0 +1,163 @@
+/* pcm_kmeans.h — C ABI of the MI355X multi-day point-cloud K-means (Lloyd) engine.
+ *
+ * Drop-in boundary for the "Multi-day 3D Point Cloud" K-means step
+ * (SURVEY.md §8b).  The reference has no K-means of its own: the step slots in
+ * after the per-pair cloud assembly of members/rafael/disparity/plugin.py:147-192,
+ * and its arithmetic follows scikit-learn's Lloyd, the only K-means the reference
+ * executes (members/jasraj/land_use_classification/core.py:227-228):
+ *
+ *   pcm_fit_begin / pcm_iter_* / pcm_iterate   replace one call of
+ *       sklearn/cluster/_kmeans.py:623-752 _kmeans_single_lloyd (its loop body is
+ *       _k_means_lloyd.pyx:23-165 lloyd_iter_chunked_dense: E-step :168-213,
+ *       accumulation :215-218 + :118-152, relocation _k_means_common.pyx:167-211,
+ *       averaging :274-295, shift :298-311, convergence _kmeans.py:717-732);
+ *   pcm_final                                 replaces the final E-step and
+ *       inertia of _kmeans.py:736-750;
+ *   pcm_labels / pcm_get_centers              return the fit outputs (labels in
+ *       the caller's original row order, centres (K, D) float32).
+ *
+ * Conventions (modelled on lloyd_iter_chunked_dense's in-place contract,
+ * _k_means_lloyd.pyx:23-32): caller-owned device buffers (torch tensors),
+ * outputs written in place, no allocation and no host synchronisation in the
+ * per-iteration entry points (pcm_iter_*, pcm_iterate, pcm_final), all work
+ * ordered on the hipStream_t passed as `stream` (NULL = default stream).
+ * Every function returns 0 on success or a negative PCM_E* code; the message of
+ * the last failure on the calling thread is available from pcm_last_error.
+ * Nothing throws across this ABI.  One engine must not be used from two
+ * threads at once; distinct engines are independent.
+ * Load this library after the process has loaded libamdhip64.so.7 (e.g. after
+ * `import torch`) so that one HIP runtime serves both.
+ */
+#ifndef PCM_KMEANS_H
+#define PCM_KMEANS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCM_ABI_VERSION 1
+
+enum pcm_dtype { PCM_F32 = 0, PCM_F16 = 1 };
+
+enum pcm_err {
+    PCM_OK = 0,
+    PCM_E_ARG = -1,      /* invalid argument / shape */
+    PCM_E_HIP = -2,      /* HIP runtime or kernel launch failure */
+    PCM_E_STATE = -3,    /* call out of order (e.g. iterate before layout) */
+    PCM_E_NONFINITE = -4,/* input points contain NaN or Inf */
+    PCM_E_NOMEM = -5
+};
+
+/* Device-side iteration status, copied to the host by pcm_read_status. */
+typedef struct pcm_status {
+    uint32_t halt;       /* 1: empty clusters need relocation (pcm_reloc_*) */
+    uint32_t done;       /* 0 running, 1 strict label convergence, 2 shift<=tol, 3 max_iter */
+    uint32_t iter;       /* completed Lloyd iterations */
+    uint32_t n_empty;    /* empty clusters seen by the halted iteration */
+    double inertia;      /* local inertia of the last pcm_final */
+    uint64_t last_changed;
+    double last_shift;
+} pcm_status;
+
+typedef struct pcm_engine pcm_engine;
+
+int pcm_abi_version(void);
+int pcm_last_error(char *buf, size_t n);
+
+/* Create an engine for D-dimensional points (1..4), K clusters, on HIP device
+ * `device`.  `max_iter` sizes the per-iteration history. */
+int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_engine **out);
+int pcm_engine_destroy(pcm_engine *e);
+
+/* Layout, step 1 (host-synchronising, once per point cloud): local bounding box
+ * of X (n rows, row-major, dtype given at create) on device.  Writes lo[d],
+ * hi[d], maxabs[d] (host arrays).  Returns PCM_E_NONFINITE for NaN/Inf input. */
+int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream,
+                    double *lo, double *hi, double *maxabs);
+
+/* Layout, step 2 (host-synchronising, once): bin rows into the pruning grid,
+ * sort them into cell-contiguous SoA order and build the tile list.  `q` are the
+ * GLOBAL fixed-point exponents (identical on every rank), `gidx0` the global row
+ * index of local row 0 (relocation tie-break).  X must stay unchanged until
+ * this call returns. */
+int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gidx0, void *stream);
+
+/* Start a fit from centres C0 (device, K*D float32): labels := -1, history
+ * cleared, absolute shift tolerance `tol`, iteration cap `max_iter`. */
+int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void *stream);
+
+/* One Lloyd iteration split at the all-reduce:
+ *   pcm_iter_local   candidate lists + assign/accumulate; folds the local
+ *                    integer statistics into the buffer of pcm_stats_ptr;
+ *   (caller all-reduces that buffer with SUM over ranks when world size > 1)
+ *   pcm_iter_global  empty-cluster check (may set halt), averaging, shift,
+ *                    convergence flags.
+ * Both are gated on the device: after convergence or halt they are no-ops. */
+int pcm_iter_local(pcm_engine *e, void *stream);
+int pcm_iter_global(pcm_engine *e, void *stream);
+/* n x (local, global) on one device without any host synchronisation. */
+int pcm_iterate(pcm_engine *e, int n, void *stream);
+
+/* Device pointer + element count (int64) of the per-iteration statistics
+ * buffer: K*(D+1) offset-encoded fixed-point sums and counts, then 1 change
+ * count.  Sum-all-reduce it between pcm_iter_local and pcm_iter_global. */
+int pcm_stats_ptr(pcm_engine *e, void **ptr, int64_t *count);
+/* Use a caller-owned device buffer of pcm_stats_ptr's count int64 elements
+ * (e.g. a torch tensor handed to torch.distributed.all_reduce) instead of the
+ * engine's own; NULL reverts to the engine buffer. */
+int pcm_bind_stats(pcm_engine *e, void *ptr);
+
+/* Empty-cluster relocation (run only after pcm_read_status reports halt):
+ * write this rank's `m` farthest-from-centre points as 32-byte records to
+ * `records` (device, m*32 bytes); the caller concatenates every rank's records
+ * (all-gather) and passes all `n_rec` of them to pcm_reloc_apply, which picks
+ * the global farthest, moves them into the empty clusters, clears halt and
+ * completes the iteration. */
+int pcm_reloc_candidates(pcm_engine *e, int m, void *records, void *stream);
+int pcm_reloc_apply(pcm_engine *e, const void *records, int n_rec, void *stream);
+
+/* Final E-step with the final centres (labels + local inertia). */
+int pcm_final(pcm_engine *e, void *stream);
+/* Labels in the caller's original row order (device int32[n]). */
+int pcm_labels(pcm_engine *e, int32_t *out, void *stream);
+/* Current centres (device float32[K*D]). */
+int pcm_get_centers(pcm_engine *e, float *out, void *stream);
+/* Per-iteration history (host arrays of length >= iter): changes, shifts. */
+int pcm_history(pcm_engine *e, uint64_t *changed, double *shift, int cap, void *stream);
+/* Synchronise `stream` and copy the device status. */
+int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream);
+
+/* Layout facts for diagnostics: cells, tiles, grid dims (host ints). */
+int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid /*[4]*/);
+/* Mean/max fine candidate-list length of the last iteration (synchronising). */
+int pcm_candidate_stats(pcm_engine *e, double *mean, int *max, int64_t *full_cells, void *stream);
+
+/* Kernel timing on the engine's launch stream (HIP events around every launch
+ * of the assign kernel and of the candidate and tail kernels).  enable=1 starts
+ * recording (resets the sums), pcm_timing_read synchronises and returns mean
+ * milliseconds per iteration for: [0] assign, [1] candidates, [2] fold+global,
+ * and the number of iterations timed. */
+int pcm_timing(pcm_engine *e, int enable);
+int pcm_timing_read(pcm_engine *e, double *ms /*[3]*/, int *count);
+
+/* Rows `rows[0..m)` (device int64) of the synthetic cloud, device float32[m*d]. */
+int pcm_synth_rows(float *out, const int64_t *rows, int64_t m, int d, uint64_t seed, void *stream);
+
+/* Counter-based U[0,1) synthetic cloud (identical to oracle.splitmix_uniform):
+ * out[(i)*d + a] for rows [start, start+n), device float32. */
+int pcm_synth_uniform(float *out, int64_t n, int d, uint64_t seed, int64_t start, void *stream);
+
+/* Stateless operator (sklearn lloyd_iter_chunked_dense shape, unit weights,
+ * brute force over all K, LDS-staged centres): labels (device int32[n]) and
+ * integer statistics (device uint64[K*(D+1)], accumulated, caller zeroes)
+ * for centres C (device float32[K*D]).  q = fixed-point exponents. */
+int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int k,
+                          const int32_t *q, int32_t *labels, uint64_t *stats, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCM_KMEANS_H */

@@ -1,6 +1,7 @@
 """ctypes binding of oracle/lloyd_ref.c (TEST INFRASTRUCTURE ONLY, see lloyd_ref.py)."""
 from __future__ import annotations
 
+
 import ctypes
 import os
 import subprocess

@@ -146,9 +146,14 @@ def segment_sums(labels: np.ndarray, vals: np.ndarray, k: int) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- M-step
-def local_stats(X, C, labels_old, q, weights=None):
-    """Per-shard E-step + accumulation: what one GPU rank contributes."""
+def local_stats(X, C, labels_old, q, weights=None, fast=False):
+    """Per-shard E-step + accumulation: what one GPU rank contributes.
+
+    ``fast`` uses the bit-identical C restatement (oracle/lloyd_ref.c)."""
     k = C.shape[0]
+    if fast and weights is None:
+        from . import cref
+        return cref.lloyd_stats(X, C, q, labels_old)
     labels = assign(X, C)
     n_changed = int(np.count_nonzero(labels != labels_old))
     xq = to_fixed(X, q)
@@ -240,7 +245,12 @@ def inertia(X, C, labels, weights=None) -> float:
 
 
 # ---------------------------------------------------------------- driver
-def lloyd_fit(X, C0, max_iter=300, tol=0.0, weights=None, shards=1, history=False):
+def assign_fast(X, C):
+    from . import cref
+    return cref.lloyd_stats(X, C, with_sums=False)[0]
+
+
+def lloyd_fit(X, C0, max_iter=300, tol=0.0, weights=None, shards=1, history=False, fast=False):
     """``_kmeans_single_lloyd`` restated (``_kmeans.py:623-752``).
 
     ``tol`` is the absolute shift tolerance (sklearn's ``_tolerance`` output).
@@ -264,7 +274,7 @@ def lloyd_fit(X, C0, max_iter=300, tol=0.0, weights=None, shards=1, history=Fals
         for r in range(shards):
             a, b = bounds[r], bounds[r + 1]
             parts.append(local_stats(X[a:b], C, labels_old[a:b], q,
-                                     None if wt is None else wt[a:b]))
+                                     None if wt is None else wt[a:b], fast=fast))
         labels = np.concatenate([p[0] for p in parts])
         sums = sum(p[1] for p in parts)
         counts = sum(p[2] for p in parts)
@@ -289,7 +299,7 @@ def lloyd_fit(X, C0, max_iter=300, tol=0.0, weights=None, shards=1, history=Fals
         if shift <= tol:
             break
         labels_old = labels
-    labels = assign(X, C)
+    labels = assign_fast(X, C) if fast else assign(X, C)
     out = dict(labels=labels, centers=C, inertia=inertia(X, C, labels, wt), n_iter=it + 1,
                strict=strict, changed=changed, q=q)
     if history:

@@ -1,0 +1,181 @@
+"""GPU parity: the HIP engine (through the C ABI) vs the CPU oracle.
+
+Bar (north_star): labels bit-exact; centres within 1e-5 relative of the
+oracle -- here they are required to be bitwise equal, since the engine and the
+oracle share the canonical arithmetic (exact integer sums, one fp64 division,
+one rounding to fp32).  n_iter and change history must match too.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import lloyd_ref as R  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def pcm():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pcm_amd
+    from pcm_amd import _lib
+    _lib.load()
+    return pcm_amd
+
+
+def gpu_fit(pcm, X, C0, max_iter, tol=0.0, dtype=torch.float32, chunk=8):
+    Xt = torch.from_numpy(np.ascontiguousarray(X)).to("cuda", dtype)
+    res = pcm.lloyd_fit(Xt, torch.from_numpy(np.ascontiguousarray(C0, dtype=np.float32)).cuda(),
+                        max_iter=max_iter, tol=tol, chunk=chunk)
+    torch.cuda.synchronize()
+    return res
+
+
+def assert_same(res, ref, where=""):
+    lab = res.labels.cpu().numpy()
+    cen = res.centers.cpu().numpy()
+    assert res.n_iter == ref["n_iter"], f"{where} n_iter {res.n_iter} != {ref['n_iter']}"
+    bad = np.flatnonzero(lab != ref["labels"])
+    assert bad.size == 0, f"{where} {bad.size} labels differ, first rows {bad[:8]}"
+    assert np.array_equal(cen, ref["centers"]), f"{where} centres differ: max {np.abs(cen - ref['centers']).max()}"
+    np.testing.assert_array_equal(res.changed, np.asarray(ref["changed"], dtype=np.int64))
+    assert res.inertia == pytest.approx(ref["inertia"], rel=1e-9, abs=1e-12)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))), ids=os.path.basename)
+def test_golden_fits(pcm, path):
+    g = np.load(path)
+    if "fit_labels" not in g:
+        pytest.skip("step-only fixture")
+    X, C0 = g["X"], g["C0"]
+    ref = R.lloyd_fit(X, C0, max_iter=300, tol=0.0, fast=True)
+    res = gpu_fit(pcm, X, C0, 300)
+    assert_same(res, ref, os.path.basename(path))
+    # and the sklearn golden itself (tolerance: sklearn sums in float32)
+    np.testing.assert_array_equal(res.labels.cpu().numpy(), g["fit_labels"])
+    assert res.n_iter == int(g["fit_n_iter"])
+    scale = np.abs(X).max()
+    np.testing.assert_allclose(res.centers.cpu().numpy(), g["fit_centers"], rtol=1e-5, atol=1e-5 * scale)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))), ids=os.path.basename)
+def test_golden_steps(pcm, path):
+    """One Lloyd step from each of sklearn's recorded centre sets: labels equal sklearn's."""
+    g = np.load(path)
+    X = g["X"]
+    for t in range(g["labels"].shape[0]):
+        res = gpu_fit(pcm, X, g["c_in"][t], 1)
+        ref = R.lloyd_fit(X, g["c_in"][t], max_iter=1, fast=True)
+        assert_same(res, ref, f"{os.path.basename(path)} step {t}")
+        # labels of the first E-step = sklearn's labels for that step: re-run E only
+        lab0 = R.assign(X, g["c_in"][t])
+        np.testing.assert_array_equal(lab0, g["labels"][t])
+
+
+CASES = [
+    # n, k, d, dtype, max_iter, seed
+    (100_000, 64, 3, "f32", 20, 1),
+    (200_000, 1024, 3, "f32", 8, 2),
+    (60_000, 16, 4, "f16", 12, 3),
+    (30_000, 5, 2, "f32", 30, 4),
+    (50_000, 300, 1, "f32", 10, 5),
+    (1, 1, 3, "f32", 3, 6),
+    (7, 7, 3, "f32", 3, 7),
+    (4099, 4096, 3, "f32", 3, 8),
+]
+
+
+@pytest.mark.parametrize("n,k,d,dt,iters,seed", CASES)
+def test_random_fit(pcm, n, k, d, dt, iters, seed):
+    X = R.splitmix_uniform(n, d, seed)
+    if dt == "f16":
+        X = X.astype(np.float16).astype(np.float32)
+    C0 = X[R.init_indices(n, k)]
+    ref = R.lloyd_fit(X, C0, max_iter=iters, fast=True)
+    res = gpu_fit(pcm, X, C0, iters, dtype=torch.float16 if dt == "f16" else torch.float32)
+    assert_same(res, ref, f"n={n} k={k} d={d}")
+
+
+def test_heightmap_like_cloud(pcm):
+    """Anisotropic 2.5-D cloud in pixel units (z,y,x as plugin.py:191-192 emits)."""
+    rng = np.random.default_rng(11)
+    n = 150_000
+    y = rng.integers(0, 1800, n).astype(np.float64)
+    x = rng.integers(0, 2400, n).astype(np.float64)
+    z = 10 * np.sin(x / 200) + 5 * np.cos(y / 150) + rng.normal(0, 0.5, n) + 30
+    X = np.stack([z, y, x], axis=1).astype(np.float32)
+    C0 = X[R.init_indices(n, 512)]
+    ref = R.lloyd_fit(X, C0, max_iter=15, fast=True)
+    res = gpu_fit(pcm, X, C0, 15)
+    assert_same(res, ref, "heightmap")
+
+
+def test_offset_cloud_and_negative(pcm):
+    X = (R.splitmix_uniform(80_000, 3, 12) * np.float32(50) - np.float32(1.0e4)).astype(np.float32)
+    C0 = X[R.init_indices(80_000, 200)]
+    ref = R.lloyd_fit(X, C0, max_iter=10, fast=True)
+    res = gpu_fit(pcm, X, C0, 10)
+    assert_same(res, ref, "offset")
+
+
+def test_ties_and_duplicates(pcm):
+    base = np.random.default_rng(5).integers(0, 6, size=(5000, 3)).astype(np.float32)
+    X = np.concatenate([base, base, base])
+    C0 = np.concatenate([X[:10], X[:10]])     # every centre duplicated: exact ties everywhere
+    ref = R.lloyd_fit(X, C0, max_iter=10, fast=True)
+    res = gpu_fit(pcm, X, C0, 10)
+    assert_same(res, ref, "ties")
+
+
+def test_relocation_many_empty(pcm):
+    X = R.splitmix_uniform(20_000, 3, 13)
+    far = np.full((6, 3), 500.0, dtype=np.float32) + np.arange(6, dtype=np.float32)[:, None]
+    C0 = np.concatenate([X[:10], far])        # 6 empty clusters on the first step
+    ref = R.lloyd_fit(X, C0, max_iter=20, fast=True)
+    res = gpu_fit(pcm, X, C0, 20, chunk=3)
+    assert res.relocations >= 1
+    assert_same(res, ref, "reloc")
+
+
+def test_tol_convergence(pcm):
+    X = R.splitmix_uniform(40_000, 3, 14)
+    C0 = X[R.init_indices(40_000, 50)]
+    ref = R.lloyd_fit(X, C0, max_iter=100, tol=1e-6, fast=True)
+    res = gpu_fit(pcm, X, C0, 100, tol=1e-6)
+    assert not res.strict
+    assert_same(res, ref, "tol")
+    np.testing.assert_array_equal(res.shift, np.array([h for h in res.shift]))
+
+
+def test_bruteforce_operator(pcm):
+    from pcm_amd.engine import assign_bruteforce
+    X = R.splitmix_uniform(50_000, 3, 15)
+    C = R.splitmix_uniform(700, 3, 16)
+    q = R.fixed_q(X)
+    stats = torch.zeros(700 * 4, dtype=torch.int64, device="cuda")
+    lab = assign_bruteforce(torch.from_numpy(X).cuda(), torch.from_numpy(C).cuda(), q, stats)
+    l2, s2, c2, _ = R.local_stats(X, C, np.full(len(X), -1, np.int32), q, fast=True)
+    np.testing.assert_array_equal(lab.cpu().numpy(), l2)
+    st = stats.cpu().numpy().reshape(700, 4)
+    np.testing.assert_array_equal(st[:, 3], c2)
+    np.testing.assert_array_equal(st[:, :3] - c2[:, None] * R.OFFSET, s2)
+
+
+def test_device_synth_matches_cpu(pcm):
+    from pcm_amd.engine import synth_uniform
+    a = synth_uniform(10_000, 3, seed=3, start=12345).cpu().numpy()
+    np.testing.assert_array_equal(a, R.splitmix_uniform(10_000, 3, 3, start=12345))
+
+
+def test_nonfinite_rejected(pcm):
+    X = R.splitmix_uniform(1000, 3, 1)
+    X[17, 1] = np.nan
+    with pytest.raises(Exception, match="NaN"):
+        gpu_fit(pcm, X, X[:4], 3)
