@@ -48,7 +48,7 @@ struct pcm_engine {
     // device buffers
     void *xs = nullptr;
     uint32_t *perm = nullptr;
-    int32_t *lab = nullptr;
+    void *lab = nullptr;             // sorted-order labels: uint16 when k <= 65535, else int32
     uint32_t *cell_start = nullptr;
     uint32_t *tile_off = nullptr;    // [ncells+1] first tile of each cell
     uint4 *tiles = nullptr;
@@ -56,6 +56,7 @@ struct pcm_engine {
     uint32_t *cc_cnt = nullptr, *cc_idx = nullptr, *fc_cnt = nullptr;
     float4 *fc_rec = nullptr;
     int32_t *fc_lab = nullptr;
+    uint8_t *fc_slot = nullptr;
     float4 *C = nullptr, *Cn = nullptr;
     unsigned long long *partials = nullptr, *stats = nullptr, *hist_changed = nullptr;
     unsigned long long *stats_own = nullptr;   // engine-owned; `stats` may point at a bound buffer
@@ -84,6 +85,14 @@ const int BBOX_BLOCKS = 1024;
 
 size_t tsize(int dtype) { return dtype == PCM_F16 ? 2 : 4; }
 
+// Internal sorted-order labels are uint16 when every label fits (saves 4 B/pt/iter of HBM).
+#ifdef PCM_DBG_LABEL32
+bool small_labels(const pcm_engine *) { return false; }
+#else
+bool small_labels(const pcm_engine *e) { return e->k <= 65535; }
+#endif
+size_t lsize(const pcm_engine *e) { return small_labels(e) ? 2 : 4; }
+
 int check_device(pcm_engine *e) {
     int cur = -1;
     HIPCHK(hipGetDevice(&cur));
@@ -111,13 +120,20 @@ int dispatch_td(int dtype, int d, F &&f) {
     return dispatch_d(d, [&](auto DD) { return f(float{}, DD); });
 }
 
+template <typename F>
+int dispatch_l(const pcm_engine *e, F &&f) {
+    if (small_labels(e)) return f(uint16_t{});
+    return f(int32_t{});
+}
+
 void free_layout(pcm_engine *e) {
     void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->cc_cnt, e->cc_idx,
-                  e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off};
+                  e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->fc_slot};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
     e->tile_off = nullptr;
+    e->fc_slot = nullptr;
     e->cc_cnt = nullptr; e->cc_idx = nullptr; e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
     e->layout_ready = false;
     e->fit_ready = false;
@@ -308,7 +324,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     const size_t ts = tsize(e->dtype);
 
     HIPCHK(hipMalloc(&e->xs, (size_t)e->d * e->npad * ts));
-    HIPCHK(hipMalloc(&e->lab, (size_t)e->npad * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&e->lab, (size_t)e->npad * lsize(e)));
     HIPCHK(hipMalloc(&e->perm, (size_t)std::max(1LL, n) * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->cell_start, (size_t)(nc + 1) * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->cc_cnt, (size_t)ncc * sizeof(uint32_t)));
@@ -316,13 +332,14 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     HIPCHK(hipMalloc(&e->fc_cnt, (size_t)nc * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->fc_rec, (size_t)nc * CAPF * sizeof(float4)));
     HIPCHK(hipMalloc(&e->fc_lab, (size_t)nc * CAPF * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&e->fc_slot, (size_t)nc * CAPF));
     HIPCHK(hipMemsetAsync(e->fc_cnt, 0, (size_t)nc * sizeof(uint32_t), s));
 
     if (n == 0) {
         HIPCHK(hipMalloc(&e->tile_off, (size_t)(nc + 1) * sizeof(uint32_t)));
         HIPCHK(hipMemsetAsync(e->tile_off, 0, (size_t)(nc + 1) * sizeof(uint32_t), s));
         HIPCHK(hipMemsetAsync(e->cell_start, 0, (size_t)(nc + 1) * sizeof(uint32_t), s));
-        HIPCHK(hipMemsetAsync(e->lab, 0xff, (size_t)e->npad * sizeof(int32_t), s));
+        HIPCHK(hipMemsetAsync(e->lab, 0xff, (size_t)e->npad * lsize(e), s));
         HIPCHK(hipMemsetAsync(e->xs, 0, (size_t)e->d * e->npad * ts, s));
         e->ntiles = 0;
         HIPCHK(hipStreamSynchronize(s));
@@ -378,7 +395,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
             using TT = decltype(T);
             constexpr int D = decltype(DD)::value;
-            k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs, e->lab);
+            k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs);
             LAUNCHCHK();
             return 0;
         });
@@ -438,8 +455,7 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
         return 0;
     });
     if (rc) return rc;
-    k_fill_i32<<<blocks_for(e->npad), 256, 0, s>>>(e->lab, e->npad, -1);
-    LAUNCHCHK();
+    HIPCHK(hipMemsetAsync(e->lab, 0xff, (size_t)e->npad * lsize(e), s));   // "no label yet" (-1 / 0xffff)
     HIPCHK(hipMemsetAsync(e->partials, 0, (size_t)NREP * e->k * (e->d + 1) * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->hist_changed, 0, (size_t)e->max_iter_cap * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->hist_shift, 0, (size_t)e->max_iter_cap * sizeof(double), s));
@@ -457,15 +473,20 @@ static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
         k_coarse<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->ctrl, gate);
         LAUNCHCHK();
         k_fine<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->fc_cnt, e->fc_rec,
-                                                    e->fc_lab, e->tile_off, e->tiles, e->ctrl, gate);
+                                                    e->fc_lab, e->fc_slot, e->tile_off, e->tiles, e->ctrl, gate);
         LAUNCHCHK();
         return 0;
     });
 }
 
-// Persistent grid: 4 resident 256-thread blocks per CU (LDS-limited), never
-// more blocks than tiles.
-static int assign_grid(pcm_engine *e) { return (int)std::min<long long>(e->ntiles, 4LL * e->num_cu); }
+// Persistent grid: as many 256-thread blocks as are co-resident (occupancy
+// query), never more blocks than tiles.
+static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, TPB, lds) != hipSuccess || per_cu < 1)
+        per_cu = 2;
+    return (int)std::min<long long>(e->ntiles, (long long)per_cu * e->num_cu);
+}
 
 static AssignArgs assign_args(pcm_engine *e) {
     AssignArgs A{};
@@ -475,6 +496,7 @@ static AssignArgs assign_args(pcm_engine *e) {
     A.ntiles = e->ntiles;
     A.fc_rec = e->fc_rec;
     A.fc_lab = e->fc_lab;
+    A.fc_slot = e->fc_slot;
     A.C = e->C;
     A.K = e->k;
     for (int a = 0; a < MAXD; ++a) A.q[a] = e->qe.q[a];
@@ -532,8 +554,14 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
         constexpr int D = decltype(DD)::value;
         if (e->ntiles > 0) {
             const size_t lds = (size_t)MSLOT * (D + 1) * TPB * sizeof(uint32_t);
-            k_assign<TT, D, 0><<<assign_grid(e), TPB, lds, s>>>(A);
-            LAUNCHCHK();
+            int rc = dispatch_l(e, [&](auto L) -> int {
+                using LT = decltype(L);
+                k_assign<TT, D, LT, 0><<<assign_grid(e, (const void *)k_assign<TT, D, LT, 0>, lds), TPB, lds, s>>>(
+                    A, e->tiles, e->fc_rec, e->fc_lab, e->fc_slot);
+                LAUNCHCHK();
+                return 0;
+            });
+            if (rc) return rc;
         }
         if (int rc = timing_mark(e, 2, s)) return rc;
         const int nf = e->k * (D + 1) + 1;
@@ -619,10 +647,13 @@ int pcm_reloc_candidates(pcm_engine *e, int m, void *records, void *stream) {
         rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
             using TT = decltype(T);
             constexpr int D = decltype(DD)::value;
-            k_reloc_keys<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)e->xs, n, e->npad, e->lab, e->perm, e->C,
-                                                             e->gidx0, k1, v1);
-            LAUNCHCHK();
-            return 0;
+            return dispatch_l(e, [&](auto L) -> int {
+                using LT = decltype(L);
+                k_reloc_keys<TT, D, LT><<<blocks_for(n), 256, 0, s>>>((const TT *)e->xs, n, e->npad,
+                                                                     (const LT *)e->lab, e->perm, e->C, e->gidx0, k1, v1);
+                LAUNCHCHK();
+                return 0;
+            });
         });
         if (rc) break;
         if ((err = rocprim::radix_sort_pairs_desc(nullptr, tb, k1, k2, v1, v2, (size_t)n, 0u, 64u, s)) ||
@@ -637,10 +668,13 @@ int pcm_reloc_candidates(pcm_engine *e, int m, void *records, void *stream) {
         rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
             using TT = decltype(T);
             constexpr int D = decltype(DD)::value;
-            k_reloc_gather<TT, D><<<blocks_for(m), 256, 0, s>>>(k2, v2, m, n, (const TT *)e->xs, e->npad, e->lab, e->qe,
-                                                               (RelocRec *)records);
-            LAUNCHCHK();
-            return 0;
+            return dispatch_l(e, [&](auto L) -> int {
+                using LT = decltype(L);
+                k_reloc_gather<TT, D, LT><<<blocks_for(m), 256, 0, s>>>(k2, v2, m, n, (const TT *)e->xs, e->npad,
+                                                                       (const LT *)e->lab, e->qe, (RelocRec *)records);
+                LAUNCHCHK();
+                return 0;
+            });
         });
         if (rc) break;
         if ((err = hipStreamSynchronize(s))) { rc = fail(PCM_E_HIP, "reloc sync"); break; }
@@ -683,8 +717,13 @@ int pcm_final(pcm_engine *e, void *stream) {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
         if (e->ntiles > 0) {
-            k_assign<TT, D, 1><<<assign_grid(e), TPB, 0, s>>>(A);
-            LAUNCHCHK();
+            return dispatch_l(e, [&](auto L) -> int {
+                using LT = decltype(L);
+                k_assign<TT, D, LT, 1><<<assign_grid(e, (const void *)k_assign<TT, D, LT, 1>, 0), TPB, 0, s>>>(
+                    A, e->tiles, e->fc_rec, e->fc_lab, e->fc_slot);
+                LAUNCHCHK();
+                return 0;
+            });
         }
         return 0;
     });
@@ -694,9 +733,12 @@ int pcm_labels(pcm_engine *e, int32_t *out, void *stream) {
     if (!e || (!out && e->n > 0)) return fail(PCM_E_ARG, "bad argument");
     if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
     if (e->n == 0) return 0;
-    k_unpermute<<<blocks_for(e->n), 256, 0, (hipStream_t)stream>>>(e->lab, e->perm, e->n, out);
-    LAUNCHCHK();
-    return 0;
+    return dispatch_l(e, [&](auto L) -> int {
+        using LT = decltype(L);
+        k_unpermute<LT><<<blocks_for(e->n), 256, 0, (hipStream_t)stream>>>((const LT *)e->lab, e->perm, e->n, out);
+        LAUNCHCHK();
+        return 0;
+    });
 }
 
 int pcm_get_centers(pcm_engine *e, float *out, void *stream) {
@@ -767,6 +809,20 @@ int pcm_synth_uniform(float *out, int64_t n, int d, uint64_t seed, int64_t start
     k_synth<<<blocks_for(n * d), 256, 0, (hipStream_t)stream>>>(out, n, d, seed, start);
     LAUNCHCHK();
     return 0;
+}
+
+// Debug (not in the public header): copy the sorted layout to device buffers.
+int pcm_debug_layout(pcm_engine *e, void *xs_out, int32_t *lab_out, uint32_t *perm_out, void *stream) {
+    if (!e || !e->layout_ready) return fail(PCM_E_STATE, "layout not built");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(xs_out, e->xs, (size_t)e->d * e->npad * tsize(e->dtype), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(perm_out, e->perm, (size_t)e->n * 4, hipMemcpyDeviceToDevice, s));
+    return dispatch_l(e, [&](auto L) -> int {
+        using LT = decltype(L);
+        k_unpermute<LT><<<blocks_for(e->n), 256, 0, s>>>((const LT *)e->lab, nullptr, e->n, lab_out);
+        LAUNCHCHK();
+        return 0;
+    });
 }
 
 int pcm_synth_rows(float *out, const int64_t *rows, int64_t m, int d, uint64_t seed, void *stream) {

@@ -24,13 +24,12 @@ namespace pcm {
 constexpr int MAXD = 4;
 constexpr int CAPC = 256;          // coarse candidate capacity
 constexpr int CAPF = 64;           // fine candidate capacity
-constexpr int MSLOT = 8;           // LDS-privatised slots per lane
+constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-centre ranks)
 constexpr int TPB = 256;           // assign block size
 constexpr int TILE = 8192;         // max points per tile (<= 63 per lane per flush)
 constexpr int NREP = 8;            // replicas of the global partials
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int QBITS = 25;
-constexpr uint32_t OFFS = 1u << QBITS;
 // Pruning margins (see DESIGN.md "Exactness of pruning").
 constexpr double PEPS = 7.62939453125e-06;   // 2^-17  >> 6 * 2^-24 (fp32 distance error)
 constexpr double PTAU = 1e-36;               // >> fp32 underflow error of a distance
@@ -81,9 +80,8 @@ __device__ __forceinline__ float comp(const float4 &c, int a) {
     return a == 0 ? c.x : a == 1 ? c.y : a == 2 ? c.z : c.w;
 }
 
-__device__ __forceinline__ uint32_t fixed_u(float x, int q) {
-    return (uint32_t)((int)__builtin_rintf(__builtin_ldexpf(x, q)) + (int)OFFS);
-}
+// Fixed-point coordinate: trunc(x * 2^q) (exact scaling, truncation toward 0).
+__device__ __forceinline__ int fixed_i(float x, int q) { return (int)__builtin_ldexpf(x, q); }
 
 __device__ __forceinline__ void decode(long long c, const int *G, int d, int *idx) {
     for (int a = d - 1; a >= 0; --a) {
@@ -209,8 +207,7 @@ __global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long lo
 // SoA gather into cell order; labels := -1
 template <typename T, int D>
 __global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long long n, long long npad,
-                                                const uint32_t *__restrict__ perm, T *__restrict__ xs,
-                                                int32_t *__restrict__ lab) {
+                                                const uint32_t *__restrict__ perm, T *__restrict__ xs) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= npad) return;
     if (i < n) {
@@ -219,7 +216,6 @@ __global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long lo
     } else {
         for (int a = 0; a < D; ++a) xs[a * npad + i] = (T)0.0f;
     }
-    lab[i] = -1;
 }
 
 // cell_start[c] = first sorted index with key >= c, for c in [0, ncells]
@@ -333,13 +329,15 @@ template <int D>
 __global__ __launch_bounds__(256) void k_fine(Grid g, const float4 *__restrict__ C, int K,
                                               const uint32_t *__restrict__ cc_cnt, const uint32_t *__restrict__ cc_idx,
                                               uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                              int32_t *__restrict__ fc_lab, const uint32_t *__restrict__ toff,
-                                              uint4 *__restrict__ tiles, const Ctrl *__restrict__ ctrl, int gate) {
+                                              int32_t *__restrict__ fc_lab, uint8_t *__restrict__ fc_slot,
+                                              const uint32_t *__restrict__ toff, uint4 *__restrict__ tiles,
+                                              const Ctrl *__restrict__ ctrl, int gate) {
     if (gate && gated(ctrl)) return;
     const long long I = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     __shared__ float4 prec[CAPC];
     __shared__ int pidx[CAPC];
+    __shared__ double cdist[4][CAPF];
     int ci[MAXD];
     decode(I, g.GC, D, ci);
     uint32_t mp = cc_cnt[I];
@@ -392,14 +390,34 @@ __global__ __launch_bounds__(256) void k_fine(Grid g, const float4 *__restrict__
             bool in = l < mp;
             float4 c = in ? (pfull ? C[l] : prec[l]) : r;
             int j = in ? (pfull ? (int)l : pidx[l]) : 0;
+#ifdef PCM_DBG_NOPRUNE_FINE
+            bool keep = in;
+#else
             bool keep = in && !prunable<D>(blo, bhi, c, r);
+#endif
             unsigned long long bal = __ballot(keep);
             uint32_t pos = total + __popcll(bal & ((1ull << lane) - 1ull));
             if (keep && pos < (uint32_t)CAPF) {
                 fc_rec[cell * CAPF + pos] = c;
                 fc_lab[cell * CAPF + pos] = j;
+                double cd = 0.0;   // squared distance to the cell centre: slot rank key
+                for (int a = 0; a < D; ++a) {
+                    double dd = 0.5 * (blo[a] + bhi[a]) - (double)comp(c, a);
+                    cd += dd * dd;
+                }
+                cdist[wv][pos] = cd;
             }
             total += __popcll(bal);
+        }
+        if (total <= (uint32_t)CAPF && (uint32_t)lane < total) {
+            // rank among the kept candidates (ties by position): nearest to the centre = slot 0
+            const double mine = cdist[wv][lane];
+            uint32_t rank = 0;
+            for (uint32_t o = 0; o < total; ++o) {
+                const double other = cdist[wv][o];
+                rank += (other < mine || (other == mine && o < (uint32_t)lane)) ? 1u : 0u;
+            }
+            fc_slot[cell * CAPF + lane] = (uint8_t)rank;
         }
         if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, toff, tiles);
     }
@@ -428,35 +446,128 @@ __device__ __forceinline__ void scan4(P rec, int mm, const float (&x)[4][D], flo
 struct AssignArgs {
     const void *xs;                 // SoA [D][npad] of T
     long long npad;
+    void *lab;                      // sorted-order labels, LT[npad] (in: previous, out: new)
     const uint4 *tiles;             // {cell, start, end, m}; m written by k_fine each iteration
     long long ntiles;
     const float4 *fc_rec;
     const int32_t *fc_lab;
+    const uint8_t *fc_slot;
     const float4 *C;                // all centres (FULL cells)
     int K;
     int q[MAXD];
-    int32_t *lab;                   // sorted-order labels (in: previous, out: new)
     unsigned long long *partials;   // [NREP][K][D+1]
     Ctrl *ctrl;
 };
 
-template <typename T> struct Vec4;
-template <> struct Vec4<float> {
-    static __device__ __forceinline__ void load(const float *p, float (&v)[4]) {
-        float4 t = *reinterpret_cast<const float4 *>(p);
-        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-    }
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void *base, unsigned long long bytes) {
+    const unsigned long long b = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    const unsigned nb = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0xffffffffull ? 0xffffffffull : bytes));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((unsigned long long)hi << 32) | lo), (short)0, (int)nb,
+                                             0x00020000);
+}
+
+// Lane-local 4 consecutive points: raw 32-bit words as loaded (fp32, or packed fp16 pairs).
+template <typename T, int D> struct Raw;
+template <int D> struct Raw<float, D> {
+    u32x4 w[D];
 };
-template <> struct Vec4<__half> {
-    static __device__ __forceinline__ void load(const __half *p, float (&v)[4]) {
-        uint2 t = *reinterpret_cast<const uint2 *>(p);
-        __half2 a = *reinterpret_cast<__half2 *>(&t.x), b = *reinterpret_cast<__half2 *>(&t.y);
-        v[0] = __low2float(a); v[1] = __high2float(a); v[2] = __low2float(b); v[3] = __high2float(b);
-    }
+template <int D> struct Raw<__half, D> {
+    u32x2 w[D];
+};
+template <typename LT> struct RawLab;
+template <> struct RawLab<uint16_t> {
+    u32x2 w;
+};
+template <> struct RawLab<int32_t> {
+    u32x4 w;
 };
 
+template <int D>
+__device__ __forceinline__ void load_x(Raw<float, D> &r, const rsrc_t *rs, unsigned off_elem) {
+    for (int a = 0; a < D; ++a) r.w[a] = __builtin_amdgcn_raw_buffer_load_b128(rs[a], off_elem * 4u, 0, 0);
+}
+#ifdef PCM_DBG_GLOBAL_LOADS
+template <int D>
+__device__ __forceinline__ void load_xg(Raw<float, D> &r, const float *xs, long long npad, unsigned off_elem) {
+    if (off_elem >= (unsigned)npad) off_elem = 0;
+    for (int a = 0; a < D; ++a) {
+        float4 v = *reinterpret_cast<const float4 *>(xs + a * npad + off_elem);
+        r.w[a][0] = __builtin_bit_cast(unsigned, v.x); r.w[a][1] = __builtin_bit_cast(unsigned, v.y);
+        r.w[a][2] = __builtin_bit_cast(unsigned, v.z); r.w[a][3] = __builtin_bit_cast(unsigned, v.w);
+    }
+}
+template <int D>
+__device__ __forceinline__ void load_xg(Raw<__half, D> &r, const float *, long long, unsigned) {}
+#define LOAD_X(dst, off) load_xg<D>(dst, (const float *)A.xs, A.npad, off)
+#else
+#define LOAD_X(dst, off) load_x<D>(dst, rx, off)
+#endif
+template <int D>
+__device__ __forceinline__ void load_x(Raw<__half, D> &r, const rsrc_t *rs, unsigned off_elem) {
+    for (int a = 0; a < D; ++a) r.w[a] = __builtin_amdgcn_raw_buffer_load_b64(rs[a], off_elem * 2u, 0, 0);
+}
+__device__ __forceinline__ void load_l(RawLab<uint16_t> &r, rsrc_t rs, unsigned off_elem) {
+    r.w = __builtin_amdgcn_raw_buffer_load_b64(rs, off_elem * 2u, 0, 0);
+}
+__device__ __forceinline__ void load_l(RawLab<int32_t> &r, rsrc_t rs, unsigned off_elem) {
+    r.w = __builtin_amdgcn_raw_buffer_load_b128(rs, off_elem * 4u, 0, 0);
+}
+template <int D>
+__device__ __forceinline__ void unpack_x(const Raw<float, D> &r, float (&x)[4][D]) {
+    for (int a = 0; a < D; ++a)
+        for (int e = 0; e < 4; ++e) {
+            // Copy the element to a scalar first: clang (ROCm 7.2) folds
+            // __builtin_bit_cast of an ext-vector element lvalue to element 0.
+            const unsigned u = r.w[a][e];
+            x[e][a] = __builtin_bit_cast(float, u);
+        }
+}
+template <int D>
+__device__ __forceinline__ void unpack_x(const Raw<__half, D> &r, float (&x)[4][D]) {
+    for (int a = 0; a < D; ++a)
+        for (int e = 0; e < 4; ++e) {
+            const unsigned word = r.w[a][e >> 1];
+            const unsigned short hb = (unsigned short)((e & 1) ? (word >> 16) : (word & 0xffffu));
+            x[e][a] = __half2float(__builtin_bit_cast(__half, hb));
+        }
+}
+__device__ __forceinline__ int lab_at(const RawLab<uint16_t> &r, int e) {
+    const unsigned word = r.w[e >> 1];
+    return (int)((e & 1) ? (word >> 16) : (word & 0xffffu));
+}
+__device__ __forceinline__ int lab_at(const RawLab<int32_t> &r, int e) { return (int)r.w[e]; }
+__device__ __forceinline__ void store_l4(rsrc_t rs, unsigned off, const int (&l)[4], const bool (&v)[4],
+                                         RawLab<uint16_t> *) {
+    if (v[0] & v[1] & v[2] & v[3]) {
+        u32x2 w;
+        w[0] = ((unsigned)l[0] & 0xffffu) | ((unsigned)l[1] << 16);
+        w[1] = ((unsigned)l[2] & 0xffffu) | ((unsigned)l[3] << 16);
+        __builtin_amdgcn_raw_buffer_store_b64(w, rs, off * 2u, 0, 0);
+    } else {
+        for (int e = 0; e < 4; ++e)
+            if (v[e]) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)l[e], rs, (off + e) * 2u, 0, 0);
+    }
+}
+__device__ __forceinline__ void store_l4(rsrc_t rs, unsigned off, const int (&l)[4], const bool (&v)[4],
+                                         RawLab<int32_t> *) {
+    if (v[0] & v[1] & v[2] & v[3]) {
+        u32x4 w;
+        for (int e = 0; e < 4; ++e) w[e] = (unsigned)l[e];
+        __builtin_amdgcn_raw_buffer_store_b128(w, rs, off * 4u, 0, 0);
+    } else {
+        for (int e = 0; e < 4; ++e)
+            if (v[e]) __builtin_amdgcn_raw_buffer_store_b32((unsigned)l[e], rs, (off + e) * 4u, 0, 0);
+    }
+}
+
 struct TileH {
-    long long cell, start, end, base0;
+    unsigned cell, start, end, base0;
     int mm, nr, full, pad_;
 };
 
@@ -465,146 +576,169 @@ __device__ __forceinline__ TileH make_hdr(const uint4 &t, int K) {
     h.cell = t.x;
     h.start = t.y;
     h.end = t.z;
+#ifdef PCM_DBG_ALLFULL
+    h.full = 1;
+#else
     h.full = (t.w == FULL) ? 1 : 0;
+#endif
     h.mm = h.full ? K : (int)t.w;
-    h.base0 = h.start & ~3LL;
+    h.base0 = h.start & ~3u;
     h.nr = (int)((h.end - h.base0 + 4 * TPB - 1) / (4 * TPB));
     return h;
 }
 
-// One lane's 4 consecutive points (SoA dwordx4 / fp16 dwordx2 per axis) + previous labels.
-template <int D>
-struct Pts {
-    float x[4][D];
-    int old[4];
-};
-
-template <typename T, int D>
-__device__ __forceinline__ void load_pts(const T *__restrict__ xs, long long npad, const int32_t *__restrict__ lab,
-                                         long long i0, long long end, Pts<D> &p) {
-    if (i0 < end) {
-        float v[4];
-        for (int a = 0; a < D; ++a) {
-            Vec4<T>::load(xs + a * npad + i0, v);
-            for (int e = 0; e < 4; ++e) p.x[e][a] = v[e];
-        }
-        const int4 o = *reinterpret_cast<const int4 *>(lab + i0);
-        p.old[0] = o.x; p.old[1] = o.y; p.old[2] = o.z; p.old[3] = o.w;
-    } else {
-        for (int e = 0; e < 4; ++e) {
-            for (int a = 0; a < D; ++a) p.x[e][a] = 0.f;
-            p.old[e] = 0;
-        }
-    }
-}
-
-// Persistent, software-pipelined assignment.  Each block walks tiles
-// blockIdx.x, +gridDim.x, ...; while it computes one round of 1024 points it
-// already has the next round (or the next tile's first round, candidate record
-// and header) in flight.  Per tile: candidates -> LDS, rounds of 4 points per
-// lane, then the LDS-privatised per-lane slot sums are folded (8 threads per
-// (slot, quantity) pair) into the global int64 partials and re-zeroed.
+// Persistent, software-pipelined assignment (one 256-thread block per slot,
+// blocks walk tiles blockIdx.x, +gridDim.x, ...).  Work item = one round of
+// 4 points per lane (1024 points) of one tile; while item k is computed the
+// loads of item k+1 (next round, or the next tile's first round and candidate
+// record) are in flight in the other register set (ping-pong, no copies).
+// Buffer loads: 32-bit offsets, out-of-range lanes read zeros (no branches).
+// Per tile: candidates in LDS (scan order = ascending centroid index, so the
+// lowest index wins ties), per-lane LDS sums for the MSLOT candidate slots
+// ranked nearest to the cell centre (k_fine), rare other winners via global
+// int64 atomics; at the tile end the slot sums are folded into the global
+// partials while the next tile's candidates are installed (2 barriers/tile).
 // MODE 0: Lloyd iteration (labels, change count, statistics); gated.
 // MODE 1: final E-step (labels + inertia); not gated by `done`.
-template <typename T, int D, int MODE>
-__global__ __launch_bounds__(TPB) void k_assign(AssignArgs A) {
+template <typename T, int D, typename LT, int MODE>
+__global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__restrict__ tiles,
+                                                const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
+                                                const uint8_t *__restrict__ fc_slot) {
     if (MODE == 0 && gated(A.ctrl)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [MSLOT][D+1][TPB]
     __shared__ float4 srec[CAPF];
     __shared__ int32_t slab[CAPF];
+    __shared__ uint8_t smap[CAPF];
+    __shared__ int32_t sinv[2][CAPF];
     const int tid = threadIdx.x;
-    long long t = blockIdx.x;
-    if (t >= A.ntiles) return;
-    const T *__restrict__ xs = reinterpret_cast<const T *>(A.xs);
+    const unsigned G = gridDim.x;
+    const unsigned nt = (unsigned)A.ntiles;
+    unsigned t = blockIdx.x;
+    if (t >= nt) return;
+    const unsigned cl = tid < CAPF ? (unsigned)tid : (unsigned)(CAPF - 1);   // candidate lane (clamped)
+#ifdef PCM_DBG_VTILES
+    auto tile_at = [&](unsigned i) {
+        const uint4 *p = tiles + (i < nt ? i : nt - 1);
+        uint4 v;
+        v.x = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(&p->x));
+        v.y = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(&p->y));
+        v.z = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(&p->z));
+        v.w = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(&p->w));
+        return v;
+    };
+#else
+    auto tile_at = [&](unsigned i) { return tiles[i < nt ? i : nt - 1]; };
+#endif
+
+    rsrc_t rx[D];
+    for (int a = 0; a < D; ++a)
+        rx[a] = make_rsrc((const T *)A.xs + (size_t)a * A.npad, (unsigned long long)A.npad * sizeof(T));
+    const rsrc_t rl = make_rsrc(A.lab, (unsigned long long)A.npad * sizeof(LT));
 
     if (MODE == 0)
         for (int e = tid; e < MSLOT * (D + 1) * TPB / 4; e += TPB)
             reinterpret_cast<uint4 *>(acc)[e] = make_uint4(0u, 0u, 0u, 0u);
 
-    // prologue: first tile's header, candidate record and first round
-    TileH h = make_hdr(A.tiles[t], A.K);
-    float4 crec = make_float4(0.f, 0.f, 0.f, 0.f);
-    int clab = 0;
-    if (!h.full && tid < h.mm) {
-        crec = A.fc_rec[h.cell * CAPF + tid];
-        clab = A.fc_lab[h.cell * CAPF + tid];
+    // Pipeline state: h = tile being computed, h1 = next tile (header known),
+    // tl2 = raw record of the tile after that; crec/clab/cslot = h1's candidates.
+    TileH h = make_hdr(tile_at(t), A.K);
+    {
+        const float4 c0 = fc_rec[(size_t)h.cell * CAPF + cl];
+        const int l0 = fc_lab[(size_t)h.cell * CAPF + cl];
+        const int s0 = fc_slot[(size_t)h.cell * CAPF + cl];
+        if (!h.full && tid < h.mm) {
+            srec[tid] = c0;
+            slab[tid] = l0;
+            smap[tid] = (uint8_t)s0;
+            sinv[0][s0] = l0;
+        }
+        if (h.full && tid < MSLOT) sinv[0][tid] = tid;
     }
-    Pts<D> cur;
-    load_pts<T, D>(xs, A.npad, A.lab, h.base0 + 4 * tid, h.end, cur);
+    TileH h1 = make_hdr(tile_at(t + G), A.K);
+    uint4 tl2 = tile_at(t + 2 * G);
+    float4 crec = fc_rec[(size_t)h1.cell * CAPF + cl];
+    int clab = fc_lab[(size_t)h1.cell * CAPF + cl];
+    int cslot = fc_slot[(size_t)h1.cell * CAPF + cl];
+
+    Raw<T, D> xa, xb;
+    RawLab<LT> la, lb_;
+    LOAD_X(xa, h.base0 + 4u * tid);
+    load_l(la, rl, h.base0 + 4u * tid);
+    __syncthreads();
 
     uint32_t nch = 0;
     double inert = 0.0;
     unsigned long long *prep = A.partials + (size_t)(blockIdx.x % NREP) * A.K * (D + 1);
-    while (true) {
-        __syncthreads();   // previous tile's readers of srec/slab/acc are done
-        if (!h.full && tid < h.mm) {
-            srec[tid] = crec;
-            slab[tid] = clab;
-        }
-        __syncthreads();
-        const long long tn = t + gridDim.x;
-        const bool has_next = tn < A.ntiles;
-        uint4 tln = make_uint4(0u, 0u, 0u, 0u);
-        if (has_next) tln = A.tiles[tn];
-        TileH hn = h;
-        for (int r = 0; r < h.nr; ++r) {
-            const long long i0 = h.base0 + (long long)r * 4 * TPB + 4 * tid;
-            Pts<D> nxt;
-            if (r + 1 < h.nr) {
-                load_pts<T, D>(xs, A.npad, A.lab, i0 + 4 * TPB, h.end, nxt);
-            } else if (has_next) {
-                hn = make_hdr(tln, A.K);
-                load_pts<T, D>(xs, A.npad, A.lab, hn.base0 + 4 * tid, hn.end, nxt);
-                if (!hn.full && tid < hn.mm) {
-                    crec = A.fc_rec[hn.cell * CAPF + tid];
-                    clab = A.fc_lab[hn.cell * CAPF + tid];
-                }
-            }
-            if (i0 < h.end) {
-                bool v[4];
-                for (int e = 0; e < 4; ++e) v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
-                float bd[4];
-                int bj[4];
-                if (h.full)
-                    scan4<D>(A.C, h.mm, cur.x, bd, bj);
-                else
-                    scan4<D>(srec, h.mm, cur.x, bd, bj);
-                int lb[4];
-                for (int e = 0; e < 4; ++e) lb[e] = h.full ? bj[e] : slab[bj[e]];
-                if (v[0] & v[1] & v[2] & v[3]) {
-                    *reinterpret_cast<int4 *>(A.lab + i0) = make_int4(lb[0], lb[1], lb[2], lb[3]);
-                } else {
-                    for (int e = 0; e < 4; ++e)
-                        if (v[e]) A.lab[i0 + e] = lb[e];
-                }
-                if (MODE == 0) {
-                    for (int e = 0; e < 4; ++e) {
-                        if (!v[e]) continue;
-                        nch += (lb[e] != cur.old[e]) ? 1u : 0u;
-#ifdef PCM_ABL_NOACC
-                        continue;
+    int r = 0;
+    int par = 0;                       // sinv parity of the current tile
+
+    // One work item (one round of h): prefetch the following item into (nx, nl)
+    // with unconditional loads, compute (cx, cl_), and at the tile's last round
+    // fold its slot sums and install h1's candidates.
+    auto step = [&](Raw<T, D> &cx, RawLab<LT> &clw, Raw<T, D> &nx, RawLab<LT> &nl) -> bool {
+        const bool last_round = (r + 1 == h.nr);
+        const bool has_next = (t + G) < nt;
+        unsigned onext = 0xfffffff0u;   // out of range: the buffer load returns zeros
+        if (!last_round)
+            onext = h.base0 + (unsigned)(r + 1) * 4u * TPB + 4u * tid;
+        else if (has_next)
+            onext = h1.base0 + 4u * tid;
+        LOAD_X(nx, onext);
+        load_l(nl, rl, onext);
+
+        const unsigned i0 = h.base0 + (unsigned)r * 4u * TPB + 4u * tid;
+        if (i0 < h.end) {
+            float x[4][D];
+            unpack_x<D>(cx, x);
+            bool v[4];
+            for (int e = 0; e < 4; ++e) v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
+            float bd[4];
+            int bj[4];
+#ifdef PCM_DBG_GREC
+            if (h.full)
+                scan4<D>(A.C, h.mm, x, bd, bj);
+            else
+                scan4<D>(fc_rec + (size_t)h.cell * CAPF, h.mm, x, bd, bj);
+#else
+            if (h.full)
+                scan4<D>(A.C, h.mm, x, bd, bj);
+            else
+                scan4<D>(srec, h.mm, x, bd, bj);
 #endif
-                        const int s = bj[e];
-                        if (s < MSLOT) {
-                            for (int a = 0; a < D; ++a)
-                                atomicAdd(&acc[(s * (D + 1) + a) * TPB + tid], fixed_u(cur.x[e][a], A.q[a]));
-                            atomicAdd(&acc[(s * (D + 1) + D) * TPB + tid], 1u);
-                        } else {
-                            unsigned long long *p = prep + (size_t)lb[e] * (D + 1);
-                            for (int a = 0; a < D; ++a)
-                                atomicAdd(p + a, (unsigned long long)fixed_u(cur.x[e][a], A.q[a]));
-                            atomicAdd(p + D, 1ull);
-                        }
+            int lbl[4];
+            for (int e = 0; e < 4; ++e) lbl[e] = h.full ? bj[e] : slab[bj[e]];
+            store_l4(rl, i0, lbl, v, (RawLab<LT> *)nullptr);
+            if (MODE == 0) {
+                for (int e = 0; e < 4; ++e) {
+                    if (!v[e]) continue;
+                    nch += (lbl[e] != lab_at(clw, e)) ? 1u : 0u;
+#ifdef PCM_ABL_NOACC
+                    continue;
+#endif
+                    const int sl = h.full ? bj[e] : (int)smap[bj[e]];
+                    if (sl < MSLOT) {
+                        for (int a = 0; a < D; ++a)
+                            atomicAdd(&acc[(sl * (D + 1) + a) * TPB + tid], (uint32_t)fixed_i(x[e][a], A.q[a]));
+                        atomicAdd(&acc[(sl * (D + 1) + D) * TPB + tid], 1u);
+                    } else {
+                        unsigned long long *p = prep + (size_t)lbl[e] * (D + 1);
+                        for (int a = 0; a < D; ++a)
+                            atomicAdd(p + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                        atomicAdd(p + D, 1ull);
                     }
-                } else {
-                    for (int e = 0; e < 4; ++e)
-                        if (v[e]) inert += (double)bd[e];
                 }
+            } else {
+                for (int e = 0; e < 4; ++e)
+                    if (v[e]) inert += (double)bd[e];
             }
-            cur = nxt;
         }
+        if (!last_round) {
+            ++r;
+            return true;
+        }
+        // ---- tile boundary: fold slot sums of h, install candidates of h1
+        __syncthreads();
         if (MODE == 0) {
-            __syncthreads();   // every lane's slot sums of this tile are in LDS
 #ifdef PCM_ABL_NOFLUSH
             const int nslots = 0;
 #else
@@ -613,27 +747,55 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A) {
             const int npairs = nslots * (D + 1);
             for (int p0 = 0; p0 < npairs; p0 += TPB / 8) {
                 const int p = p0 + tid / 8, sub = tid & 7;
-                unsigned long long s = 0;
+                long long sacc = 0;
                 if (p < npairs)
                     for (int k = 0; k < TPB / 8; ++k) {
-                        uint32_t *a = &acc[p * TPB + sub + 8 * k];
-                        s += *a;
-                        *a = 0u;   // re-zero for the next tile (same thread, no race)
+                        uint32_t *ap = &acc[p * TPB + sub + 8 * k];
+                        // per-lane sums are exact int32 (<= 63 points of |xq| < 2^25)
+                        sacc += (p % (D + 1) == D) ? (long long)*ap : (long long)(int32_t)*ap;
+                        *ap = 0u;
                     }
-                s += __shfl_down(s, 4, 8);
-                s += __shfl_down(s, 2, 8);
-                s += __shfl_down(s, 1, 8);
-                if (p < npairs && sub == 0 && s) {
+                sacc += __shfl_down(sacc, 4, 8);
+                sacc += __shfl_down(sacc, 2, 8);
+                sacc += __shfl_down(sacc, 1, 8);
+                if (p < npairs && sub == 0 && sacc) {
                     const int slot = p / (D + 1), qq = p % (D + 1);
-                    const int lbl = h.full ? slot : slab[slot];
-                    atomicAdd(prep + (size_t)lbl * (D + 1) + qq, s);
+                    atomicAdd(prep + (size_t)sinv[par][slot] * (D + 1) + qq, (unsigned long long)sacc);
                 }
             }
         }
-        if (!has_next) break;
-        t = tn;
-        h = hn;
+        if (!has_next) return false;
+        if (!h1.full && tid < h1.mm) {
+            srec[tid] = crec;
+            slab[tid] = clab;
+            smap[tid] = (uint8_t)cslot;
+            sinv[par ^ 1][cslot] = clab;
+        }
+        if (h1.full && tid < MSLOT) sinv[par ^ 1][tid] = tid;
+        par ^= 1;
+        h = h1;
+        t += G;
+        r = 0;
+        h1 = make_hdr(tl2, A.K);
+        tl2 = tile_at(t + 2 * G);
+        crec = fc_rec[(size_t)h1.cell * CAPF + cl];
+        clab = fc_lab[(size_t)h1.cell * CAPF + cl];
+        cslot = fc_slot[(size_t)h1.cell * CAPF + cl];
+        __syncthreads();
+        return true;
+    };
+#ifdef PCM_DBG_NO_PINGPONG
+    while (true) {
+        if (!step(xa, la, xb, lb_)) break;
+        xa = xb;
+        la = lb_;
     }
+#else
+    while (true) {
+        if (!step(xa, la, xb, lb_)) break;
+        if (!step(xb, lb_, xa, la)) break;
+    }
+#endif
 
     if (MODE == 0) {
         for (int o = 32; o > 0; o >>= 1) nch += __shfl_xor(nch, o);
@@ -721,8 +883,7 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
         float out[4] = {0.f, 0.f, 0.f, 0.f};
         if (c > 0) {
             for (int a = 0; a < D; ++a) {
-                const long long sraw = (long long)stats[(size_t)j * (D + 1) + a];
-                const long long sv = sraw - (long long)c * (long long)OFFS;
+                const long long sv = (long long)stats[(size_t)j * (D + 1) + a];   // exact signed sum
                 const double m = ((double)sv * __builtin_ldexp(1.0, -q[a])) / (double)c;
                 out[a] = (float)m;
             }
@@ -776,16 +937,16 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
 
 // ------------------------------------------------------------------ relocation
 // key = dist_bits << 32 | (0xffffffff - global index); sort descending.
-template <typename T, int D>
+template <typename T, int D, typename LT>
 __global__ __launch_bounds__(256) void k_reloc_keys(const T *__restrict__ xs, long long n, long long npad,
-                                                    const int32_t *__restrict__ lab, const uint32_t *__restrict__ perm,
+                                                    const LT *__restrict__ lab, const uint32_t *__restrict__ perm,
                                                     const float4 *__restrict__ C, long long gidx0,
                                                     unsigned long long *__restrict__ keys, uint32_t *__restrict__ vals) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= n) return;
     float x[D];
     for (int a = 0; a < D; ++a) x[a] = to_f<T>(xs[a * npad + i]);
-    float d = dist_canon<D>(x, C[lab[i]]);
+    float d = dist_canon<D>(x, C[(int)lab[i]]);
     unsigned long long g = (unsigned long long)(gidx0 + perm[i]);
     keys[i] = ((unsigned long long)__float_as_uint(d) << 32) | (0xffffffffull - (g & 0xffffffffull));
     vals[i] = (uint32_t)i;
@@ -798,9 +959,9 @@ struct RelocRec {
     int32_t xq[4];
 };
 
-template <typename T, int D>
+template <typename T, int D, typename LT>
 __global__ void k_reloc_gather(const unsigned long long *__restrict__ keys, const uint32_t *__restrict__ vals, int m,
-                               long long n, const T *__restrict__ xs, long long npad, const int32_t *__restrict__ lab,
+                               long long n, const T *__restrict__ xs, long long npad, const LT *__restrict__ lab,
                                QExp qe, RelocRec *__restrict__ out) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= m) return;
@@ -810,9 +971,9 @@ __global__ void k_reloc_gather(const unsigned long long *__restrict__ keys, cons
     if (t < n) {
         uint32_t i = vals[t];
         r.key = keys[t];
-        r.label = lab[i];
+        r.label = (int)lab[i];
         r.valid = 1;
-        for (int a = 0; a < D; ++a) r.xq[a] = (int)fixed_u(to_f<T>(xs[a * npad + i]), qe.q[a]) - (int)OFFS;
+        for (int a = 0; a < D; ++a) r.xq[a] = fixed_i(to_f<T>(xs[a * npad + i]), qe.q[a]);
     }
     out[t] = r;
 }
@@ -854,7 +1015,7 @@ __global__ __launch_bounds__(256) void k_reloc_apply(const RelocRec *__restrict_
                 unsigned long long *so = stats + (size_t)r.label * (D + 1);
                 unsigned long long *sn = stats + (size_t)j * (D + 1);
                 for (int a = 0; a < D; ++a) {
-                    unsigned long long u = (unsigned long long)(long long)(r.xq[a] + (int)OFFS);
+                    unsigned long long u = (unsigned long long)(long long)r.xq[a];
                     so[a] -= u;
                     sn[a] = u;
                 }
@@ -869,10 +1030,11 @@ __global__ __launch_bounds__(256) void k_reloc_apply(const RelocRec *__restrict_
 }
 
 // ------------------------------------------------------------------ misc
-__global__ __launch_bounds__(256) void k_unpermute(const int32_t *__restrict__ lab, const uint32_t *__restrict__ perm,
+template <typename LT>
+__global__ __launch_bounds__(256) void k_unpermute(const LT *__restrict__ lab, const uint32_t *__restrict__ perm,
                                                    long long n, int32_t *__restrict__ out) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i < n) out[perm[i]] = lab[i];
+    if (i < n) out[perm ? perm[i] : (uint32_t)i] = (int32_t)lab[i];
 }
 
 template <int D>
@@ -957,7 +1119,7 @@ __global__ __launch_bounds__(256) void k_bruteforce(const float *__restrict__ X,
         labels[i] = bj;
         if (stats) {
             unsigned long long *p = stats + (size_t)bj * (D + 1);
-            for (int a = 0; a < D; ++a) atomicAdd(p + a, (unsigned long long)fixed_u(x[a], qe.q[a]));
+            for (int a = 0; a < D; ++a) atomicAdd(p + a, (unsigned long long)(long long)fixed_i(x[a], qe.q[a]));
             atomicAdd(p + D, 1ull);
         }
     }

@@ -1,10 +1,11 @@
 """Fixed-point scale of the exact centroid sums (product side).
 
-Each coordinate enters the per-cluster sums as ``xq = rint(ldexp(x, q_a))``
-with ``q_a = QBITS - e_a`` where ``max|x_a| < 2**e_a`` over the WHOLE cloud (all
-ranks), so ``|xq| < 2**QBITS``.  The kernels keep ``xq + 2**QBITS`` per lane in
-uint32 and all sums in int64, which makes the centroid update independent of
-summation order, block order and GPU count.
+Each coordinate enters the per-cluster sums as ``xq = trunc(ldexp(x, q_a))``
+(exact power-of-two scaling, truncation toward zero) with ``q_a = QBITS - e_a``
+where ``max|x_a| < 2**e_a`` over the WHOLE cloud (all ranks), so
+``|xq| < 2**QBITS``.  The kernels keep per-lane partial sums of at most 63
+points in int32 and every other sum in int64, which makes the centroid update
+independent of summation order, block order and GPU count.
 """
 from __future__ import annotations
 

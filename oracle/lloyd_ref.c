@@ -33,7 +33,7 @@ static inline float dist_canon(const float *x, const float *c, int d) {
 
 /* labels[i] = argmin_j dist(x_i, c_j); also counts changes vs labels_old
  * (nullable) and, when sums/counts are non-null, accumulates exact int64
- * fixed-point sums: xq = rint(ldexpf(x, q[a])).  Returns n_changed. */
+ * fixed-point sums: xq = trunc(ldexpf(x, q[a])).  Returns n_changed. */
 int64_t ref_lloyd_stats(const float *X, int64_t n, int d, const float *C, int k,
                         const int32_t *q, const int32_t *labels_old,
                         int32_t *labels, int64_t *sums, int64_t *counts,
@@ -119,7 +119,7 @@ int64_t ref_lloyd_stats(const float *X, int64_t n, int d, const float *C, int k,
                 if (ms) {
                     mc[lab] += 1;
                     for (int t = 0; t < d; ++t)
-                        ms[(size_t)lab * d + t] += (int64_t)rintf(ldexpf(xs[t][p], q[t]));
+                        ms[(size_t)lab * d + t] += (int64_t)ldexpf(xs[t][p], q[t]);   /* trunc */
                 }
             }
         }

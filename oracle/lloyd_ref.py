@@ -29,9 +29,10 @@ so that labels can be bit-exact between CPU and GPU:
   (sklearn evaluates ``||c||^2 - 2 x.c`` through a GEMM, ``_k_means_lloyd.pyx:196-203``,
   which differs from the direct form on ~1e-5 of near-tie labels);
 * argmin: strict ``<`` scanning centroids in index order (``:205-213``);
-* accumulation: exact int64 fixed point, ``xq = rint(ldexp(x, q_a))`` with a
-  per-dimension ``q_a = QBITS - e_a`` where ``max|x_a| < 2**e_a``; the result is
-  independent of summation order, block order and GPU count;
+* accumulation: exact int64 fixed point, ``xq = trunc(ldexp(x, q_a))`` (exact
+  power-of-two scaling, truncation toward zero) with a per-dimension
+  ``q_a = QBITS - e_a`` where ``max|x_a| < 2**e_a``; the result is independent
+  of summation order, block order and GPU count;
 * update: ``c = float32(float64(S) * 2**-q / float64(count))``;
 * empty clusters: sklearn's farthest-point relocation with a deterministic
   order (distance descending, then global point index ascending); a cluster
@@ -49,8 +50,7 @@ from __future__ import annotations
 
 import numpy as np
 
-QBITS = 25          # |xq| < 2**QBITS; GPU lanes hold (xq + 2**QBITS) in uint32
-OFFSET = 1 << QBITS
+QBITS = 25          # |xq| < 2**QBITS; GPU lanes hold per-lane partial sums in int32
 CHUNK = 8192        # rows per distance block (memory bound only)
 SHIFT_LANES = 1024  # lanes of the GPU finalize reduction tree
 
@@ -121,7 +121,7 @@ def assign(X: np.ndarray, C: np.ndarray) -> np.ndarray:
 
 # ---------------------------------------------------------------- fixed point
 def fixed_q(X: np.ndarray) -> np.ndarray:
-    """Per-dimension fixed-point exponent q_a with |rint(ldexp(x, q_a))| < 2**QBITS."""
+    """Per-dimension fixed-point exponent q_a with |trunc(ldexp(x, q_a))| < 2**QBITS."""
     maxabs = np.max(np.abs(X), axis=0).astype(np.float64) if X.shape[0] else np.zeros(X.shape[1])
     _, e = np.frexp(maxabs)
     e = np.where(maxabs == 0, 0, e)
@@ -129,7 +129,7 @@ def fixed_q(X: np.ndarray) -> np.ndarray:
 
 
 def to_fixed(X: np.ndarray, q: np.ndarray) -> np.ndarray:
-    return np.rint(np.ldexp(X, q.astype(np.int32)[None, :])).astype(np.int64)
+    return np.ldexp(X, q.astype(np.int32)[None, :]).astype(np.int64)   # truncates toward zero
 
 
 def segment_sums(labels: np.ndarray, vals: np.ndarray, k: int) -> np.ndarray:
