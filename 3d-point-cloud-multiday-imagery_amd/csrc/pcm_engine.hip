@@ -69,6 +69,7 @@ struct pcm_engine {
     unsigned long long *cand_stats = nullptr;
     int *rank_buf = nullptr;
     int rank_cap = 0;
+    int *empty_idx = nullptr;        // [K] scratch of the relocation kernel
     Ctrl ctrl_host{};
     // optional kernel timing: event pairs per iteration, summed on read
     static constexpr int TEV = 64;
@@ -245,6 +246,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->nonfinite, sizeof(unsigned));
     err = err ? err : hipMalloc(&e->bbox_out, 2 * MAXD * sizeof(double));
     err = err ? err : hipMalloc(&e->cand_stats, 3 * sizeof(unsigned long long));
+    err = err ? err : hipMalloc(&e->empty_idx, (size_t)k * sizeof(int));
     err = err ? err : hipMemset(e->partials, 0, (size_t)NREP * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMemset(e->ctrl, 0, sizeof(Ctrl));
     if (err != hipSuccess) {
@@ -262,7 +264,7 @@ int pcm_engine_destroy(pcm_engine *e) {
             if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
     free_layout(e);
     void *ps[] = {e->C, e->Cn, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
-                  e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf};
+                  e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -289,7 +291,7 @@ int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream, doubl
         constexpr int D = decltype(DD)::value;
         k_bbox_partial<TT, D><<<nblk, 256, 0, s>>>((const TT *)X, n, e->bbox_part, e->nonfinite);
         LAUNCHCHK();
-        k_bbox_final<D><<<1, 64, 0, s>>>(e->bbox_part, nblk, e->bbox_out);
+        k_bbox_final<D><<<1, 256, 0, s>>>(e->bbox_part, nblk, e->bbox_out);
         LAUNCHCHK();
         return 0;
     });
@@ -472,7 +474,10 @@ static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
         constexpr int D = decltype(DD)::value;
         k_coarse<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->ctrl, gate);
         LAUNCHCHK();
-        k_fine<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->fc_cnt, e->fc_rec,
+        int nchild = 1;
+        for (int a = 0; a < D; ++a) nchild *= e->g.F;
+        const long long fblocks = e->g.ncoarse * ((nchild + FINE_WAVES - 1) / FINE_WAVES);
+        k_fine<D><<<(int)fblocks, 64 * FINE_WAVES, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->fc_cnt, e->fc_rec,
                                                     e->fc_lab, e->fc_slot, e->tile_off, e->tiles, e->ctrl, gate);
         LAUNCHCHK();
         return 0;
@@ -696,7 +701,8 @@ int pcm_reloc_apply(pcm_engine *e, const void *records, int n_rec, void *stream)
     }
     int rc = dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_reloc_apply<D><<<1, 256, 0, s>>>((const RelocRec *)records, n_rec, e->held, e->k, e->rank_buf, e->ctrl);
+        k_reloc_apply<D><<<1, 256, 0, s>>>((const RelocRec *)records, n_rec, e->held, e->k, e->rank_buf,
+                                           e->empty_idx, e->ctrl);
         LAUNCHCHK();
         return 0;
     });

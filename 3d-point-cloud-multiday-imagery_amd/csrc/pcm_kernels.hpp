@@ -174,18 +174,33 @@ __global__ __launch_bounds__(256) void k_bbox_partial(const T *__restrict__ X, l
 }
 
 template <int D>
-__global__ void k_bbox_final(const float *__restrict__ part, int nblk, double *__restrict__ out) {
-    // out: lo[D], hi[D]
-    if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(256) void k_bbox_final(const float *__restrict__ part, int nblk, double *__restrict__ out) {
+    // out: lo[D], hi[D]; one block, strided per-thread pass then an LDS tree
+    __shared__ float smn[D][256], smx[D][256];
+    const int tid = threadIdx.x;
     for (int a = 0; a < D; ++a) {
         float mn = __builtin_inff(), mx = -__builtin_inff();
-        for (int b = 0; b < nblk; ++b) {
+        for (int b = tid; b < nblk; b += 256) {
             mn = fminf(mn, part[(size_t)b * 2 * D + a]);
             mx = fmaxf(mx, part[(size_t)b * 2 * D + D + a]);
         }
-        out[a] = mn;
-        out[D + a] = mx;
+        smn[a][tid] = mn;
+        smx[a][tid] = mx;
     }
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (tid < st)
+            for (int a = 0; a < D; ++a) {
+                smn[a][tid] = fminf(smn[a][tid], smn[a][tid + st]);
+                smx[a][tid] = fmaxf(smx[a][tid], smx[a][tid + st]);
+            }
+        __syncthreads();
+    }
+    if (tid == 0)
+        for (int a = 0; a < D; ++a) {
+            out[a] = smn[a][0];
+            out[D + a] = smx[a][0];
+        }
 }
 
 template <typename T, int D>
@@ -324,103 +339,118 @@ __device__ __forceinline__ void publish_m(long long cell, uint32_t m, uint32_t *
     for (uint32_t o = toff[cell]; o < toff[cell + 1]; ++o) tiles[o].w = m;
 }
 
-// One block per coarse cell; each wave refines children using the parent list.
+// Fine candidate lists: one wave per fine cell, FINE_WAVES cells of the same
+// coarse parent per block (the parent list is staged in LDS once per block).
+// Reference r = the parent candidate nearest the cell centre (any centroid is
+// a valid reference; only the pruning test needs the fp64 margins).  Kept
+// candidates stay in ascending centroid order; each also gets its rank by
+// distance to the cell centre (slot 0 = nearest) for the assign kernel's
+// LDS-privatised sums.
+constexpr int FINE_WAVES = 4;
+
 template <int D>
-__global__ __launch_bounds__(256) void k_fine(Grid g, const float4 *__restrict__ C, int K,
-                                              const uint32_t *__restrict__ cc_cnt, const uint32_t *__restrict__ cc_idx,
-                                              uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                              int32_t *__restrict__ fc_lab, uint8_t *__restrict__ fc_slot,
-                                              const uint32_t *__restrict__ toff, uint4 *__restrict__ tiles,
-                                              const Ctrl *__restrict__ ctrl, int gate) {
+__global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *__restrict__ C, int K,
+                                                          const uint32_t *__restrict__ cc_cnt,
+                                                          const uint32_t *__restrict__ cc_idx,
+                                                          uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
+                                                          int32_t *__restrict__ fc_lab, uint8_t *__restrict__ fc_slot,
+                                                          const uint32_t *__restrict__ toff, uint4 *__restrict__ tiles,
+                                                          const Ctrl *__restrict__ ctrl, int gate) {
     if (gate && gated(ctrl)) return;
-    const long long I = blockIdx.x;
+    int nchild = 1;
+    for (int a = 0; a < D; ++a) nchild *= g.F;
+    const int bpc = (nchild + FINE_WAVES - 1) / FINE_WAVES;      // blocks per coarse cell
+    const long long I = blockIdx.x / bpc;
+    const int ch = (blockIdx.x % bpc) * FINE_WAVES + (threadIdx.x >> 6);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     __shared__ float4 prec[CAPC];
     __shared__ int pidx[CAPC];
-    __shared__ double cdist[4][CAPF];
+    __shared__ float cdist[FINE_WAVES][CAPF];
     int ci[MAXD];
     decode(I, g.GC, D, ci);
     uint32_t mp = cc_cnt[I];
     const bool pfull = (mp == FULL);
     if (pfull) mp = (uint32_t)K;
     if (!pfull)
-        for (uint32_t l = tid; l < mp; l += 256) {
-            int j = (int)cc_idx[I * CAPC + l];
+        for (uint32_t l = tid; l < mp; l += 64 * FINE_WAVES) {
+            const int j = (int)cc_idx[I * CAPC + l];
             pidx[l] = j;
             prec[l] = C[j];
         }
     __syncthreads();
-    int nch = 1;
-    for (int a = 0; a < D; ++a) nch *= g.F;
-    for (int ch = wv; ch < nch; ch += 4) {
-        int o[MAXD], f[MAXD];
+    if (ch >= nchild) return;
+    int f[MAXD];
+    {
         int t = ch;
-        bool ok = true;
         for (int a = D - 1; a >= 0; --a) {
-            o[a] = t % g.F;
+            f[a] = ci[a] * g.F + t % g.F;
             t /= g.F;
-            f[a] = ci[a] * g.F + o[a];
-            ok &= f[a] < g.G[a];
+            if (f[a] >= g.G[a]) return;   // wave-uniform
         }
-        if (!ok) continue;
-        const long long cell = encode(f, g.G, D);
-        if (!g.prune) {
-            if (lane == 0) publish_m(cell, FULL, fc_cnt, toff, tiles);
-            continue;
-        }
-        double blo[MAXD], bhi[MAXD];
-        cell_box(g, f, f, blo, bhi);
-        double best = __builtin_inf();
-        int bj = 0x7fffffff;
-        for (uint32_t l = lane; l < mp; l += 64) {
-            float4 c = pfull ? C[l] : prec[l];
-            int j = pfull ? (int)l : pidx[l];
-            double m = maxdist<D>(blo, bhi, c);
-            if (m < best) { best = m; bj = j; }
-        }
-        for (int s = 32; s > 0; s >>= 1) {
-            double ob = __shfl_xor(best, s);
-            int oj = __shfl_xor(bj, s);
-            if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
-        }
-        const float4 r = C[bj];
-        uint32_t total = 0;
-        for (uint32_t base = 0; base < mp; base += 64) {
-            uint32_t l = base + lane;
-            bool in = l < mp;
-            float4 c = in ? (pfull ? C[l] : prec[l]) : r;
-            int j = in ? (pfull ? (int)l : pidx[l]) : 0;
-#ifdef PCM_DBG_NOPRUNE_FINE
-            bool keep = in;
-#else
-            bool keep = in && !prunable<D>(blo, bhi, c, r);
-#endif
-            unsigned long long bal = __ballot(keep);
-            uint32_t pos = total + __popcll(bal & ((1ull << lane) - 1ull));
-            if (keep && pos < (uint32_t)CAPF) {
-                fc_rec[cell * CAPF + pos] = c;
-                fc_lab[cell * CAPF + pos] = j;
-                double cd = 0.0;   // squared distance to the cell centre: slot rank key
-                for (int a = 0; a < D; ++a) {
-                    double dd = 0.5 * (blo[a] + bhi[a]) - (double)comp(c, a);
-                    cd += dd * dd;
-                }
-                cdist[wv][pos] = cd;
-            }
-            total += __popcll(bal);
-        }
-        if (total <= (uint32_t)CAPF && (uint32_t)lane < total) {
-            // rank among the kept candidates (ties by position): nearest to the centre = slot 0
-            const double mine = cdist[wv][lane];
-            uint32_t rank = 0;
-            for (uint32_t o = 0; o < total; ++o) {
-                const double other = cdist[wv][o];
-                rank += (other < mine || (other == mine && o < (uint32_t)lane)) ? 1u : 0u;
-            }
-            fc_slot[cell * CAPF + lane] = (uint8_t)rank;
-        }
-        if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, toff, tiles);
     }
+    const long long cell = encode(f, g.G, D);
+    if (!g.prune) {
+        if (lane == 0) publish_m(cell, FULL, fc_cnt, toff, tiles);
+        return;
+    }
+    double blo[MAXD], bhi[MAXD];
+    cell_box(g, f, f, blo, bhi);
+    float ctr[MAXD];
+    for (int a = 0; a < D; ++a) ctr[a] = (float)(0.5 * (blo[a] + bhi[a]));
+    // reference: nearest parent candidate to the centre (fp32, lowest index on ties)
+    float best = __builtin_inff();
+    int bj = 0x7fffffff;
+    for (uint32_t l = lane; l < mp; l += 64) {
+        const float4 c = pfull ? C[l] : prec[l];
+        const int j = pfull ? (int)l : pidx[l];
+        float dsum = 0.f;
+        for (int a = 0; a < D; ++a) {
+            const float dd = ctr[a] - comp(c, a);
+            dsum += dd * dd;
+        }
+        if (dsum < best || (dsum == best && j < bj)) { best = dsum; bj = j; }
+    }
+    for (int sft = 32; sft > 0; sft >>= 1) {
+        const float ob = __shfl_xor(best, sft);
+        const int oj = __shfl_xor(bj, sft);
+        if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+    }
+    const float4 r = C[bj];
+    uint32_t total = 0;
+    for (uint32_t base = 0; base < mp; base += 64) {
+        const uint32_t l = base + lane;
+        const bool in = l < mp;
+        const float4 c = in ? (pfull ? C[l] : prec[l]) : r;
+        const int j = in ? (pfull ? (int)l : pidx[l]) : 0;
+#ifdef PCM_DBG_NOPRUNE_FINE
+        const bool keep = in;
+#else
+        const bool keep = in && !prunable<D>(blo, bhi, c, r);
+#endif
+        const unsigned long long bal = __ballot(keep);
+        const uint32_t pos = total + __popcll(bal & ((1ull << lane) - 1ull));
+        if (keep && pos < (uint32_t)CAPF) {
+            fc_rec[cell * CAPF + pos] = c;
+            fc_lab[cell * CAPF + pos] = j;
+            float cd = 0.f;
+            for (int a = 0; a < D; ++a) {
+                const float dd = ctr[a] - comp(c, a);
+                cd += dd * dd;
+            }
+            cdist[wv][pos] = cd;
+        }
+        total += __popcll(bal);
+    }
+    if (total <= (uint32_t)CAPF && (uint32_t)lane < total) {
+        const float mine = cdist[wv][lane];
+        uint32_t rank = 0;
+        for (uint32_t o = 0; o < total; ++o) {
+            const float other = cdist[wv][o];
+            rank += (other < mine || (other == mine && o < (uint32_t)lane)) ? 1u : 0u;
+        }
+        fc_slot[cell * CAPF + lane] = (uint8_t)rank;
+    }
+    if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, toff, tiles);
 }
 
 // ------------------------------------------------------------------ assign
@@ -983,7 +1013,8 @@ __global__ void k_reloc_gather(const unsigned long long *__restrict__ keys, cons
 template <int D>
 __global__ __launch_bounds__(256) void k_reloc_apply(const RelocRec *__restrict__ recs, int nrec,
                                                      unsigned long long *__restrict__ stats, int K,
-                                                     int *__restrict__ rank_buf, Ctrl *__restrict__ ctrl) {
+                                                     int *__restrict__ rank_buf, int *__restrict__ empty_idx,
+                                                     Ctrl *__restrict__ ctrl) {
     const int tid = threadIdx.x;
     // rank of each valid record by (key desc); keys are globally unique
     for (int i = tid; i < nrec; i += 256) {
@@ -1004,9 +1035,15 @@ __global__ __launch_bounds__(256) void k_reloc_apply(const RelocRec *__restrict_
             if (rank_buf[i] == 0) top = i;
         bool doit = top >= 0 && (recs[top].key >> 32) != 0ull;
         if (doit) {
+            // the empty clusters are fixed before any move (sklearn iterates a
+            // precomputed list, _k_means_common.pyx:177-178): a donor cluster
+            // emptied by a move is not refilled in this pass
+            int n_empty = 0;
+            for (int j = 0; j < K; ++j)
+                if (stats[(size_t)j * (D + 1) + D] == 0ull) empty_idx[n_empty++] = j;
             int done_moves = 0;
-            for (int j = 0; j < K; ++j) {
-                if (stats[(size_t)j * (D + 1) + D] != 0ull) continue;
+            for (int ei = 0; ei < n_empty; ++ei) {
+                const int j = empty_idx[ei];
                 int pick = -1;
                 for (int i = 0; i < nrec; ++i)
                     if (rank_buf[i] == done_moves) { pick = i; break; }

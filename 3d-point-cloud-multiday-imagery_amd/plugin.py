@@ -1,0 +1,148 @@
+"""Drop-in "Multi-day 3D Point Cloud" plugin with the GPU K-means fusion step.
+
+Boundary: the reference's ``HeightMapExtractor``
+(members/rafael/disparity/plugin.py:22-243) builds one point cloud per stereo
+pair -- ``points_coords = stack([z, y, x])`` (plugin.py:191-192) emitted as a
+napari points layer (plugin.py:220-233) -- and never fuses days.  This class
+keeps that component's public contract:
+
+* ``name == "Multi-day 3D Point Cloud"`` (plugin.py:32-34; viewer.py:475-476
+  dispatches the rafael tab on ``"3D Point Cloud" in plugin.name``);
+* ``requires_image = False`` (plugin.py:29-30, read by viewer.py:107);
+* ``run(kml_path, is_debug_mode=True, is_debug_pair=False,
+  is_one_random_pair=True, n=10)`` (plugin.py:36-40, defaults from
+  constants.py:5-10), called on a napari worker thread (widget.py:144-147);
+* returns host numpy layers only, and never raises: failures come back as an
+  error image layer (plugin.py:77-79, 89-91, 236-241).
+
+``run`` delegates the per-pair stereo pipeline to the reference extractor (or
+any object with the same ``run``), keeps every layer it returns, and appends
+the fused result of the K-means step that slots in after plugin.py:192:
+a centroid points layer and the fused cloud with a per-point ``cluster``
+property.  The K-means itself is ``pcm_amd.lloyd_fit`` on the GPU; extra
+knobs (K, iterations, tolerance) are constructor arguments so ``run``'s
+signature stays the reference's (viewer.py:118-127 would turn extra ``run``
+parameters into file pickers).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+try:  # inside the reference tree: the real plugin ABC
+    from interface import SatellitePlugin  # type: ignore
+except Exception:  # headless / tests
+    from ._interface import SatellitePlugin
+
+PREFIX = "[Multi-day 3D Point Cloud]"
+CLOUD_LAYER_SUFFIX = "3D Point Cloud"
+DEFAULTS = dict(is_debug_mode=True, is_debug_pair=False, is_one_random_pair=True, n=10)
+
+_gpu_lock = threading.Lock()   # one fit at a time per process (widgets may run concurrently)
+
+
+def _tolerance(X: np.ndarray, tol: float) -> float:
+    """sklearn ``_tolerance`` (_kmeans.py:279-287): mean per-axis variance x tol."""
+    if tol == 0 or X.shape[0] == 0:
+        return 0.0
+    return float(np.mean(np.var(X.astype(np.float64), axis=0)) * tol)
+
+
+def _gpu_fit(X: np.ndarray, C0: np.ndarray, max_iter: int, tol_abs: float):
+    import torch
+
+    from .lloyd import lloyd_fit
+
+    with _gpu_lock:
+        Xt = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).cuda()
+        Ct = torch.from_numpy(np.ascontiguousarray(C0, dtype=np.float32)).cuda()
+        res = lloyd_fit(Xt, Ct, max_iter=max_iter, tol=tol_abs)
+        torch.cuda.synchronize()
+        return (res.labels.cpu().numpy(), res.centers.cpu().numpy(), float(res.inertia), int(res.n_iter))
+
+
+def _norm(v: np.ndarray) -> np.ndarray:
+    """Height property as the reference builds it: 2/98 percentiles -> [0, 1] (plugin.py:181-188)."""
+    if v.size == 0:
+        return v.astype(np.float64)
+    lo, hi = np.percentile(v, 2), np.percentile(v, 98)
+    return np.clip((v - lo) / (hi - lo + 1e-6), 0.0, 1.0)
+
+
+def kmeans_fuse(clouds: Sequence[np.ndarray], n_clusters: int = 1024, max_iter: int = 300, tol: float = 1e-4,
+                seed: int = 1, fit: Optional[Callable] = None):
+    """Fuse per-pair (M_i, 3) z,y,x clouds into one K-means reconstruction.
+
+    Returns (layers, result) where ``result`` has labels (N,), centers (K, 3),
+    inertia, n_iter.  Init: rows ``sorted(default_rng(seed).choice(N, K))``
+    (SURVEY.md §8d); K is clipped to N.
+    """
+    clouds = [np.asarray(c, dtype=np.float64).reshape(-1, 3) for c in clouds if np.asarray(c).size]
+    if not clouds:
+        raise ValueError("no point cloud layers to fuse")
+    X = np.concatenate(clouds).astype(np.float32)          # boundary cast
+    n = X.shape[0]
+    k = int(min(n_clusters, n))
+    idx = np.sort(np.random.default_rng(seed).choice(n, k, replace=False))
+    C0 = X[idx]
+    labels, centers, inertia, n_iter = (fit or _gpu_fit)(X, C0, int(max_iter), _tolerance(X, tol))
+    counts = np.bincount(labels, minlength=k)
+    layers = [
+        (centers.astype(np.float64),
+         {"name": f"{PREFIX} Fused K-means Centroids", "size": 4,
+          "properties": {"height": _norm(centers[:, 0].astype(np.float64)), "count": counts},
+          "scale": (1, 1, 1), "opacity": 1.0, "face_colormap": "turbo", "face_color": "height"},
+         "points"),
+        (X.astype(np.float64),
+         {"name": f"{PREFIX} Fused {CLOUD_LAYER_SUFFIX}", "size": 2,
+          "properties": {"cluster": labels.astype(np.int32), "height": _norm(X[:, 0].astype(np.float64))},
+          "scale": (1, 1, 1), "opacity": 0.8, "face_colormap": "turbo", "face_color": "cluster"},
+         "points"),
+    ]
+    return layers, dict(labels=labels, centers=centers, inertia=inertia, n_iter=n_iter, n_points=n)
+
+
+class HeightMapExtractor(SatellitePlugin):
+    """Multi-day 3D point clouds from WV3 stereo pairs, fused by GPU K-means."""
+
+    requires_image = False
+
+    def __init__(self, base=None, n_clusters: int = 1024, max_iter: int = 300, tol: float = 1e-4,
+                 fit: Optional[Callable] = None):
+        self._base = base
+        self.n_clusters = n_clusters
+        self.max_iter = max_iter
+        self.tol = tol
+        self._fit = fit
+        self.last_result = None
+
+    @property
+    def name(self):
+        return "Multi-day 3D Point Cloud"
+
+    def _base_extractor(self):
+        if self._base is None:
+            # the reference's per-pair pipeline (members/rafael/disparity/plugin.py:22)
+            from members.rafael.disparity.plugin import HeightMapExtractor as RefExtractor  # type: ignore
+            self._base = RefExtractor()
+        return self._base
+
+    def run(self, kml_path, is_debug_mode: bool = DEFAULTS["is_debug_mode"],
+            is_debug_pair: bool = DEFAULTS["is_debug_pair"],
+            is_one_random_pair: bool = DEFAULTS["is_one_random_pair"], n: int = DEFAULTS["n"]) -> List:
+        try:
+            layers = list(self._base_extractor().run(kml_path, is_debug_mode=is_debug_mode,
+                                                     is_debug_pair=is_debug_pair,
+                                                     is_one_random_pair=is_one_random_pair, n=n))
+            clouds = [data for data, params, kind in layers
+                      if kind == "points" and str(params.get("name", "")).endswith(CLOUD_LAYER_SUFFIX)]
+            if not clouds:   # the pipeline returned only images (or an error layer): pass it through
+                return layers
+            fused, self.last_result = kmeans_fuse(clouds, self.n_clusters, self.max_iter, self.tol, fit=self._fit)
+            return layers + fused
+        except Exception as e:   # reference convention: an error layer, never an exception
+            import traceback
+            traceback.print_exc()
+            return [(np.ones((100, 100)), {"name": f"Error: {e}"}, "image")]

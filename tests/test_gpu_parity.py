@@ -179,3 +179,26 @@ def test_nonfinite_rejected(pcm):
     X[17, 1] = np.nan
     with pytest.raises(Exception, match="NaN"):
         gpu_fit(pcm, X, X[:4], 3)
+
+
+def test_relocation_donor_emptied(pcm):
+    X = np.array([[0.0, 0, 0], [0.1, 0, 0], [0.2, 0, 0], [100.0, 0, 0]], np.float32)
+    C0 = np.array([[1000.0, 0, 0], [0.0, 0, 0], [90.0, 0, 0]], np.float32)
+    ref = R.lloyd_fit(X, C0, max_iter=5)
+    res = gpu_fit(pcm, X, C0, 5, chunk=1)
+    assert res.relocations >= 1
+    assert_same(res, ref, "donor")
+
+
+def test_plugin_gpu_matches_oracle(pcm):
+    from fake_pipeline import SyntheticPairExtractor
+    plugin = pcm.HeightMapExtractor(base=SyntheticPairExtractor(n_pairs=3, shape=(90, 120)), n_clusters=64,
+                                    max_iter=30, tol=0.0)
+    layers = plugin.run("roi.kml")
+    fused = [l for l in layers if "Fused" in l[1]["name"]]
+    assert len(fused) == 2
+    X = fused[1][0].astype(np.float32)
+    C0 = X[R.init_indices(X.shape[0], 64)]
+    ref = R.lloyd_fit(X, C0, max_iter=30, fast=True)
+    np.testing.assert_array_equal(fused[1][1]["properties"]["cluster"], ref["labels"])
+    np.testing.assert_array_equal(fused[0][0].astype(np.float32), ref["centers"])

@@ -146,3 +146,19 @@ def test_splitmix_deterministic_and_uniform():
     np.testing.assert_array_equal(a[500:510], b)
     assert 0.0 <= a.min() and a.max() < 1.0
     assert abs(float(a.mean()) - 0.5) < 0.02
+
+
+def test_relocation_donor_emptied_is_not_refilled():
+    """The empty list is fixed before moves (_k_means_common.pyx:177-178): the
+    donor of the farthest point (cluster 2, a singleton) becomes empty and must
+    take the largest cluster's centre, not another point."""
+    X = np.array([[0.0], [0.1], [0.2], [100.0]], np.float32)
+    C0 = np.array([[1000.0], [0.0], [90.0]], np.float32)
+    q = R.fixed_q(X)
+    lab, sums, cnt, _ = R.local_stats(X, C0, np.full(4, -1, np.int32), q)
+    np.testing.assert_array_equal(cnt, [0, 3, 1])
+    R.relocate(sums, cnt, R.far_candidates(X, C0, lab, 0, 1), q)
+    np.testing.assert_array_equal(cnt, [1, 3, 0])
+    Cn = R.average(sums, cnt, q, C0)
+    assert Cn[0, 0] == np.float32(100.0)
+    assert Cn[2, 0] == Cn[1, 0]

@@ -1,0 +1,78 @@
+"""CPU plumbing of the drop-in plugin (SURVEY config 1: ~10k-point synthetic
+cloud, K=8, no GPU).  The K-means backend is injected: the oracle here (the
+product has no CPU fallback); the GPU path is tests/test_gpu_parity.py."""
+import inspect
+
+import numpy as np
+import pytest
+
+import pcm_amd
+from fake_pipeline import SyntheticPairExtractor
+from oracle import lloyd_ref as R
+
+
+def oracle_fit(X, C0, max_iter, tol_abs):
+    r = R.lloyd_fit(X, C0, max_iter=max_iter, tol=tol_abs)
+    return r["labels"], r["centers"], r["inertia"], r["n_iter"]
+
+
+def test_contract_matches_reference_component():
+    p = pcm_amd.HeightMapExtractor()
+    assert p.name == "Multi-day 3D Point Cloud" and "3D Point Cloud" in p.name   # viewer.py:475
+    assert p.requires_image is False and p.requires_viewer is False
+    sig = inspect.signature(p.run)
+    assert list(sig.parameters) == ["kml_path", "is_debug_mode", "is_debug_pair", "is_one_random_pair", "n"]
+    assert [sig.parameters[k].default for k in list(sig.parameters)[1:]] == [True, False, True, 10]
+
+
+def test_config1_plumbing_cpu():
+    base = SyntheticPairExtractor(n_pairs=1, shape=(100, 100))   # ~9k valid points
+    plugin = pcm_amd.HeightMapExtractor(base=base, n_clusters=8, max_iter=300, tol=1e-4, fit=oracle_fit)
+    layers = plugin.run("roi.kml", n=1)
+    assert all(isinstance(l, tuple) and len(l) == 3 for l in layers)
+    names = [l[1]["name"] for l in layers]
+    assert names[-2:] == ["[Multi-day 3D Point Cloud] Fused K-means Centroids",
+                          "[Multi-day 3D Point Cloud] Fused 3D Point Cloud"]
+    cent, cloud = layers[-2], layers[-1]
+    assert cent[2] == "points" and cent[0].shape == (8, 3)
+    assert cloud[0].shape[0] == plugin.last_result["n_points"] > 8000
+    lab = cloud[1]["properties"]["cluster"]
+    assert lab.shape == (cloud[0].shape[0],) and lab.max() < 8
+    # the result equals a direct oracle fit of the same fused cloud
+    X = cloud[0].astype(np.float32)
+    ref = R.lloyd_fit(X, X[R.init_indices(X.shape[0], 8)], max_iter=300,
+                      tol=float(np.mean(np.var(X.astype(np.float64), axis=0)) * 1e-4))
+    np.testing.assert_array_equal(lab, ref["labels"])
+    np.testing.assert_array_equal(cent[0].astype(np.float32), ref["centers"])
+
+
+def test_multi_pair_fusion_keeps_reference_layers():
+    base = SyntheticPairExtractor(n_pairs=3, shape=(60, 80))
+    plugin = pcm_amd.HeightMapExtractor(base=base, n_clusters=16, fit=oracle_fit)
+    layers = plugin.run("roi.kml")
+    ref_layers = base.run("roi.kml")
+    assert len(layers) == len(ref_layers) + 2
+    assert sum(l[0].shape[0] for l in ref_layers if l[2] == "points") == layers[-1][0].shape[0]
+
+
+def test_errors_become_error_layer():
+    def boom(*a, **k):
+        raise RuntimeError("HIP extension missing")
+    plugin = pcm_amd.HeightMapExtractor(base=SyntheticPairExtractor(), fit=boom)
+    out = plugin.run("roi.kml")
+    assert len(out) == 1 and out[0][2] == "image" and out[0][1]["name"].startswith("Error:")
+
+
+def test_base_error_layer_passes_through():
+    plugin = pcm_amd.HeightMapExtractor(base=SyntheticPairExtractor(fail=True), fit=oracle_fit)
+    out = plugin.run("roi.kml")
+    assert out[0][1]["name"] == "Error: synthetic failure"
+
+
+def test_gpu_path_fails_loudly_without_device():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    plugin = pcm_amd.HeightMapExtractor(base=SyntheticPairExtractor(n_pairs=1, shape=(40, 40)), n_clusters=4)
+    out = plugin.run("roi.kml")
+    assert out[0][1]["name"].startswith("Error:")
