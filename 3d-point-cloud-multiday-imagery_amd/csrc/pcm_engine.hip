@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -54,6 +55,7 @@ struct pcm_engine {
     uint4 *tiles = nullptr;
     int num_cu = 256;
     uint32_t *cc_cnt = nullptr, *cc_idx = nullptr, *fc_cnt = nullptr;
+    float4 *cc_rec = nullptr;
     float4 *fc_rec = nullptr;
     int32_t *fc_lab = nullptr;
     uint8_t *fc_slot = nullptr;
@@ -129,12 +131,13 @@ int dispatch_l(const pcm_engine *e, F &&f) {
 
 void free_layout(pcm_engine *e) {
     void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->cc_cnt, e->cc_idx,
-                  e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->fc_slot};
+                  e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->fc_slot, e->cc_rec};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
     e->tile_off = nullptr;
     e->fc_slot = nullptr;
+    e->cc_rec = nullptr;
     e->cc_cnt = nullptr; e->cc_idx = nullptr; e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
     e->layout_ready = false;
     e->fit_ready = false;
@@ -321,6 +324,9 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     e->gidx0 = gidx0;
     const long long n = e->n;
     e->npad = ((n + 3) / 4) * 4 + 4;
+    // the assign kernel addresses points with 32-bit offsets and uses offset
+    // 0x0ffffff0 (points) as its always-out-of-range prefetch
+    if (e->npad >= 0x0ffffff0LL) return fail(PCM_E_ARG, "at most 2^28 - 32 points per engine (shard larger clouds)");
     choose_grid(e);
     const long long nc = e->g.ncells, ncc = e->g.ncoarse;
     const size_t ts = tsize(e->dtype);
@@ -331,6 +337,9 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     HIPCHK(hipMalloc(&e->cell_start, (size_t)(nc + 1) * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->cc_cnt, (size_t)ncc * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->cc_idx, (size_t)ncc * CAPC * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->cc_rec, (size_t)ncc * CAPC * sizeof(float4)));
+    HIPCHK(hipMemsetAsync(e->cc_idx, 0, (size_t)ncc * CAPC * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(e->cc_rec, 0, (size_t)ncc * CAPC * sizeof(float4), s));
     HIPCHK(hipMalloc(&e->fc_cnt, (size_t)nc * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->fc_rec, (size_t)nc * CAPF * sizeof(float4)));
     HIPCHK(hipMalloc(&e->fc_lab, (size_t)nc * CAPF * sizeof(int32_t)));
@@ -472,12 +481,14 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
 static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_coarse<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->ctrl, gate);
+        k_coarse<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->cc_rec, e->ctrl,
+                                                      gate);
         LAUNCHCHK();
         int nchild = 1;
         for (int a = 0; a < D; ++a) nchild *= e->g.F;
         const long long fblocks = e->g.ncoarse * ((nchild + FINE_WAVES - 1) / FINE_WAVES);
-        k_fine<D><<<(int)fblocks, 64 * FINE_WAVES, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->fc_cnt, e->fc_rec,
+        k_fine<D><<<(int)fblocks, 64 * FINE_WAVES, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->cc_rec,
+                                                           e->fc_cnt, e->fc_rec,
                                                     e->fc_lab, e->fc_slot, e->tile_off, e->tiles, e->ctrl, gate);
         LAUNCHCHK();
         return 0;
@@ -490,6 +501,7 @@ static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, TPB, lds) != hipSuccess || per_cu < 1)
         per_cu = 2;
+    if (const char *ov = std::getenv("PCM_ASSIGN_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(ov));
     return (int)std::min<long long>(e->ntiles, (long long)per_cu * e->num_cu);
 }
 

@@ -227,9 +227,9 @@ __global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long lo
     if (i >= npad) return;
     if (i < n) {
         long long s = perm[i];
-        for (int a = 0; a < D; ++a) xs[a * npad + i] = X[s * D + a];
+        for (int a = 0; a < D; ++a) xs[i * D + a] = X[s * D + a];
     } else {
-        for (int a = 0; a < D; ++a) xs[a * npad + i] = (T)0.0f;
+        for (int a = 0; a < D; ++a) xs[i * D + a] = (T)0.0f;
     }
 }
 
@@ -274,6 +274,7 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
 template <int D>
 __global__ __launch_bounds__(256) void k_coarse(Grid g, const float4 *__restrict__ C, int K,
                                                 uint32_t *__restrict__ cc_cnt, uint32_t *__restrict__ cc_idx,
+                                                float4 *__restrict__ cc_rec,
                                                 const Ctrl *__restrict__ ctrl, int gate) {
     if (gate && gated(ctrl)) return;
     const long long I = blockIdx.x;
@@ -324,7 +325,10 @@ __global__ __launch_bounds__(256) void k_coarse(Grid g, const float4 *__restrict
         uint32_t woff = 0;
         for (int w = 0; w < wv; ++w) woff += wcnt[w];
         uint32_t pos = total + woff + pre;
-        if (keep && pos < (uint32_t)CAPC) cc_idx[I * CAPC + pos] = (uint32_t)j;
+        if (keep && pos < (uint32_t)CAPC) {
+            cc_idx[I * CAPC + pos] = (uint32_t)j;
+            cc_rec[I * CAPC + pos] = C[j];
+        }
         total += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
         __syncthreads();
     }
@@ -333,10 +337,10 @@ __global__ __launch_bounds__(256) void k_coarse(Grid g, const float4 *__restrict
 
 // A cell's candidate count goes to fc_cnt and into the .w of each of its tiles
 // (so the assign kernel reaches its candidates in one dependent load).
-__device__ __forceinline__ void publish_m(long long cell, uint32_t m, uint32_t *fc_cnt, const uint32_t *toff,
-                                          uint4 *tiles) {
+__device__ __forceinline__ void publish_m(long long cell, uint32_t m, uint32_t *fc_cnt, uint32_t o0, uint32_t o1,
+                                           uint4 *tiles) {
     fc_cnt[cell] = m;
-    for (uint32_t o = toff[cell]; o < toff[cell + 1]; ++o) tiles[o].w = m;
+    for (uint32_t o = o0; o < o1; ++o) tiles[o].w = m;
 }
 
 // Fine candidate lists: one wave per fine cell, FINE_WAVES cells of the same
@@ -352,6 +356,7 @@ template <int D>
 __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *__restrict__ C, int K,
                                                           const uint32_t *__restrict__ cc_cnt,
                                                           const uint32_t *__restrict__ cc_idx,
+                                                          const float4 *__restrict__ cc_rec,
                                                           uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
                                                           int32_t *__restrict__ fc_lab, uint8_t *__restrict__ fc_slot,
                                                           const uint32_t *__restrict__ toff, uint4 *__restrict__ tiles,
@@ -369,14 +374,13 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
     int ci[MAXD];
     decode(I, g.GC, D, ci);
     uint32_t mp = cc_cnt[I];
+    // the parent list is loaded speculatively (all CAPC slots, one level of loads)
+    for (uint32_t l = tid; l < (uint32_t)CAPC; l += 64 * FINE_WAVES) {
+        pidx[l] = (int)cc_idx[I * CAPC + l];
+        prec[l] = cc_rec[I * CAPC + l];
+    }
     const bool pfull = (mp == FULL);
     if (pfull) mp = (uint32_t)K;
-    if (!pfull)
-        for (uint32_t l = tid; l < mp; l += 64 * FINE_WAVES) {
-            const int j = (int)cc_idx[I * CAPC + l];
-            pidx[l] = j;
-            prec[l] = C[j];
-        }
     __syncthreads();
     if (ch >= nchild) return;
     int f[MAXD];
@@ -389,8 +393,9 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
         }
     }
     const long long cell = encode(f, g.G, D);
+    const uint32_t to0 = toff[cell], to1 = toff[cell + 1];   // issued early, used at the end
     if (!g.prune) {
-        if (lane == 0) publish_m(cell, FULL, fc_cnt, toff, tiles);
+        if (lane == 0) publish_m(cell, FULL, fc_cnt, to0, to1, tiles);
         return;
     }
     double blo[MAXD], bhi[MAXD];
@@ -399,23 +404,22 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
     for (int a = 0; a < D; ++a) ctr[a] = (float)(0.5 * (blo[a] + bhi[a]));
     // reference: nearest parent candidate to the centre (fp32, lowest index on ties)
     float best = __builtin_inff();
-    int bj = 0x7fffffff;
+    int bj = 0x7fffffff;   // list position of the reference (positions ascend with centroid index)
     for (uint32_t l = lane; l < mp; l += 64) {
         const float4 c = pfull ? C[l] : prec[l];
-        const int j = pfull ? (int)l : pidx[l];
         float dsum = 0.f;
         for (int a = 0; a < D; ++a) {
             const float dd = ctr[a] - comp(c, a);
             dsum += dd * dd;
         }
-        if (dsum < best || (dsum == best && j < bj)) { best = dsum; bj = j; }
+        if (dsum < best || (dsum == best && (int)l < bj)) { best = dsum; bj = (int)l; }
     }
     for (int sft = 32; sft > 0; sft >>= 1) {
         const float ob = __shfl_xor(best, sft);
         const int oj = __shfl_xor(bj, sft);
         if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
     }
-    const float4 r = C[bj];
+    const float4 r = pfull ? C[bj] : prec[bj];
     uint32_t total = 0;
     for (uint32_t base = 0; base < mp; base += 64) {
         const uint32_t l = base + lane;
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
         }
         fc_slot[cell * CAPF + lane] = (uint8_t)rank;
     }
-    if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, toff, tiles);
+    if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, to0, to1, tiles);
 }
 
 // ------------------------------------------------------------------ assign
@@ -474,7 +478,7 @@ __device__ __forceinline__ void scan4(P rec, int mm, const float (&x)[4][D], flo
 }
 
 struct AssignArgs {
-    const void *xs;                 // SoA [D][npad] of T
+    const void *xs;                 // packed AoS [npad][D] of T, cell order
     long long npad;
     void *lab;                      // sorted-order labels, LT[npad] (in: previous, out: new)
     const uint4 *tiles;             // {cell, start, end, m}; m written by k_fine each iteration
@@ -502,13 +506,11 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void *base, unsigned long long
                                              0x00020000);
 }
 
-// Lane-local 4 consecutive points: raw 32-bit words as loaded (fp32, or packed fp16 pairs).
-template <typename T, int D> struct Raw;
-template <int D> struct Raw<float, D> {
-    u32x4 w[D];
-};
-template <int D> struct Raw<__half, D> {
-    u32x2 w[D];
+// Lane-local 4 consecutive points in the packed AoS layout ([npad][D] of T):
+// 4*D*sizeof(T) bytes = NW 32-bit words, loaded as b128 pieces (+ a b64 tail).
+template <typename T, int D> struct Raw {
+    static constexpr int NW = 4 * D * (int)sizeof(T) / 4;
+    unsigned w[NW];
 };
 template <typename LT> struct RawLab;
 template <> struct RawLab<uint16_t> {
@@ -518,30 +520,21 @@ template <> struct RawLab<int32_t> {
     u32x4 w;
 };
 
-template <int D>
-__device__ __forceinline__ void load_x(Raw<float, D> &r, const rsrc_t *rs, unsigned off_elem) {
-    for (int a = 0; a < D; ++a) r.w[a] = __builtin_amdgcn_raw_buffer_load_b128(rs[a], off_elem * 4u, 0, 0);
-}
-#ifdef PCM_DBG_GLOBAL_LOADS
-template <int D>
-__device__ __forceinline__ void load_xg(Raw<float, D> &r, const float *xs, long long npad, unsigned off_elem) {
-    if (off_elem >= (unsigned)npad) off_elem = 0;
-    for (int a = 0; a < D; ++a) {
-        float4 v = *reinterpret_cast<const float4 *>(xs + a * npad + off_elem);
-        r.w[a][0] = __builtin_bit_cast(unsigned, v.x); r.w[a][1] = __builtin_bit_cast(unsigned, v.y);
-        r.w[a][2] = __builtin_bit_cast(unsigned, v.z); r.w[a][3] = __builtin_bit_cast(unsigned, v.w);
+// off_pt = index of the lane's first point; one descriptor for the whole AoS array.
+template <typename T, int D>
+__device__ __forceinline__ void load_x(Raw<T, D> &r, rsrc_t rs, unsigned off_pt) {
+    constexpr int NW = Raw<T, D>::NW;
+    const unsigned boff = off_pt * (unsigned)(D * sizeof(T));
+    for (int k = 0; k + 4 <= NW; k += 4) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff + 4u * k, 0, 0);
+        r.w[k] = v[0]; r.w[k + 1] = v[1]; r.w[k + 2] = v[2]; r.w[k + 3] = v[3];
+    }
+    if (NW % 4 == 2) {
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, boff + 4u * (NW - 2), 0, 0);
+        r.w[NW - 2] = v[0]; r.w[NW - 1] = v[1];
     }
 }
-template <int D>
-__device__ __forceinline__ void load_xg(Raw<__half, D> &r, const float *, long long, unsigned) {}
-#define LOAD_X(dst, off) load_xg<D>(dst, (const float *)A.xs, A.npad, off)
-#else
-#define LOAD_X(dst, off) load_x<D>(dst, rx, off)
-#endif
-template <int D>
-__device__ __forceinline__ void load_x(Raw<__half, D> &r, const rsrc_t *rs, unsigned off_elem) {
-    for (int a = 0; a < D; ++a) r.w[a] = __builtin_amdgcn_raw_buffer_load_b64(rs[a], off_elem * 2u, 0, 0);
-}
+#define LOAD_X(dst, off) load_x<T, D>(dst, rx, off)
 __device__ __forceinline__ void load_l(RawLab<uint16_t> &r, rsrc_t rs, unsigned off_elem) {
     r.w = __builtin_amdgcn_raw_buffer_load_b64(rs, off_elem * 2u, 0, 0);
 }
@@ -550,21 +543,17 @@ __device__ __forceinline__ void load_l(RawLab<int32_t> &r, rsrc_t rs, unsigned o
 }
 template <int D>
 __device__ __forceinline__ void unpack_x(const Raw<float, D> &r, float (&x)[4][D]) {
-    for (int a = 0; a < D; ++a)
-        for (int e = 0; e < 4; ++e) {
-            // Copy the element to a scalar first: clang (ROCm 7.2) folds
-            // __builtin_bit_cast of an ext-vector element lvalue to element 0.
-            const unsigned u = r.w[a][e];
-            x[e][a] = __builtin_bit_cast(float, u);
-        }
+    for (int e = 0; e < 4; ++e)
+        for (int a = 0; a < D; ++a) x[e][a] = __uint_as_float(r.w[e * D + a]);
 }
 template <int D>
 __device__ __forceinline__ void unpack_x(const Raw<__half, D> &r, float (&x)[4][D]) {
-    for (int a = 0; a < D; ++a)
-        for (int e = 0; e < 4; ++e) {
-            const unsigned word = r.w[a][e >> 1];
-            const unsigned short hb = (unsigned short)((e & 1) ? (word >> 16) : (word & 0xffffu));
-            x[e][a] = __half2float(__builtin_bit_cast(__half, hb));
+    for (int e = 0; e < 4; ++e)
+        for (int a = 0; a < D; ++a) {
+            const int k = e * D + a;
+            const unsigned word = r.w[k >> 1];
+            const unsigned short hb = (unsigned short)((k & 1) ? (word >> 16) : (word & 0xffffu));
+            x[e][a] = __half2float(__ushort_as_half(hb));
         }
 }
 __device__ __forceinline__ int lab_at(const RawLab<uint16_t> &r, int e) {
@@ -660,9 +649,7 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
     auto tile_at = [&](unsigned i) { return tiles[i < nt ? i : nt - 1]; };
 #endif
 
-    rsrc_t rx[D];
-    for (int a = 0; a < D; ++a)
-        rx[a] = make_rsrc((const T *)A.xs + (size_t)a * A.npad, (unsigned long long)A.npad * sizeof(T));
+    const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     const rsrc_t rl = make_rsrc(A.lab, (unsigned long long)A.npad * sizeof(LT));
 
     if (MODE == 0)
@@ -708,7 +695,7 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
     auto step = [&](Raw<T, D> &cx, RawLab<LT> &clw, Raw<T, D> &nx, RawLab<LT> &nl) -> bool {
         const bool last_round = (r + 1 == h.nr);
         const bool has_next = (t + G) < nt;
-        unsigned onext = 0xfffffff0u;   // out of range: the buffer load returns zeros
+        unsigned onext = 0x0ffffff0u;   // out of range (x D*sizeof(T) bytes): the buffer load returns zeros
         if (!last_round)
             onext = h.base0 + (unsigned)(r + 1) * 4u * TPB + 4u * tid;
         else if (has_next)
@@ -724,7 +711,9 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
             for (int e = 0; e < 4; ++e) v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
             float bd[4];
             int bj[4];
-#ifdef PCM_DBG_GREC
+#ifdef PCM_ABL_NOCOMPUTE
+            for (int e = 0; e < 4; ++e) { bd[e] = x[e][0]; bj[e] = (x[e][D - 1] > 0.5f) ? 1 : 0; }
+#elif defined(PCM_DBG_GREC)
             if (h.full)
                 scan4<D>(A.C, h.mm, x, bd, bj);
             else
@@ -742,7 +731,7 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
                 for (int e = 0; e < 4; ++e) {
                     if (!v[e]) continue;
                     nch += (lbl[e] != lab_at(clw, e)) ? 1u : 0u;
-#ifdef PCM_ABL_NOACC
+#if defined(PCM_ABL_NOACC) || defined(PCM_ABL_NOCOMPUTE)
                     continue;
 #endif
                     const int sl = h.full ? bj[e] : (int)smap[bj[e]];
@@ -888,7 +877,11 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
     sarg[tid] = barg;
     __syncthreads();
     const uint32_t resume = ctrl->resume;
+#ifdef PCM_ABL_NOCOMPUTE
+    if (false) {   // ablation build: never halt (statistics are meaningless)
+#else
     if (cnt_empty > 0 && !resume) {
+#endif
         // Snapshot the reduced statistics: the no-op iterations queued behind a
         // halt still run their all-reduce on `stats`.
         for (int i = tid; i < K * (D + 1) + 1; i += 1024) held[i] = stats[i];
@@ -960,6 +953,9 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
         if (changed == 0ull) done = 1u;
         else if (shift <= ctrl->tol) done = 2u;
         ctrl->iter = it + 1;
+#ifdef PCM_ABL_NOCOMPUTE
+        done = 0u;
+#endif
         if (!done && it + 1 >= ctrl->max_iter) done = 3u;
         ctrl->done = done;
     }
@@ -975,7 +971,7 @@ __global__ __launch_bounds__(256) void k_reloc_keys(const T *__restrict__ xs, lo
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= n) return;
     float x[D];
-    for (int a = 0; a < D; ++a) x[a] = to_f<T>(xs[a * npad + i]);
+    for (int a = 0; a < D; ++a) x[a] = to_f<T>(xs[i * D + a]);
     float d = dist_canon<D>(x, C[(int)lab[i]]);
     unsigned long long g = (unsigned long long)(gidx0 + perm[i]);
     keys[i] = ((unsigned long long)__float_as_uint(d) << 32) | (0xffffffffull - (g & 0xffffffffull));
@@ -1003,7 +999,7 @@ __global__ void k_reloc_gather(const unsigned long long *__restrict__ keys, cons
         r.key = keys[t];
         r.label = (int)lab[i];
         r.valid = 1;
-        for (int a = 0; a < D; ++a) r.xq[a] = fixed_i(to_f<T>(xs[a * npad + i]), qe.q[a]);
+        for (int a = 0; a < D; ++a) r.xq[a] = fixed_i(to_f<T>(xs[i * D + a]), qe.q[a]);
     }
     out[t] = r;
 }
