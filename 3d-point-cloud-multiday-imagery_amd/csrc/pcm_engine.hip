@@ -59,7 +59,8 @@ struct pcm_engine {
     float4 *fc_rec = nullptr;
     int32_t *fc_lab = nullptr;
     uint8_t *fc_slot = nullptr;
-    float4 *C = nullptr, *Cn = nullptr;
+    float4 *C = nullptr, *Cn = nullptr, *Cold = nullptr;
+    double *scratch_d = nullptr;
     unsigned long long *partials = nullptr, *stats = nullptr, *hist_changed = nullptr;
     unsigned long long *stats_own = nullptr;   // engine-owned; `stats` may point at a bound buffer
     unsigned long long *held = nullptr;        // statistics of a halted iteration
@@ -151,6 +152,7 @@ void choose_grid(pcm_engine *e) {
     g.d = e->d;
     g.F = 4;
     double target = std::min(32.0 * e->k, (double)e->n / 1024.0);
+    if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     target = std::max(1.0, std::min(target, (double)(1 << 18)));
     double vol = 1.0;
     int nondeg = 0;
@@ -238,6 +240,9 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     hipError_t err = hipSuccess;
     err = err ? err : hipMalloc(&e->C, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
+    err = err ? err : hipMalloc(&e->Cold, (size_t)k * sizeof(float4));
+    err = err ? err : hipMemset(e->Cold, 0, (size_t)k * sizeof(float4));
+    err = err ? err : hipMalloc(&e->scratch_d, sizeof(double));
     err = err ? err : hipMalloc(&e->partials, (size_t)NREP * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
     e->stats = e->stats_own;
@@ -266,7 +271,7 @@ int pcm_engine_destroy(pcm_engine *e) {
         for (int j = 0; j < 4; ++j)
             if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
     free_layout(e);
-    void *ps[] = {e->C, e->Cn, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
+    void *ps[] = {e->C, e->Cn, e->Cold, e->scratch_d, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
                   e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx};
     for (void *p : ps)
         if (p) (void)hipFree(p);
@@ -341,9 +346,13 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     HIPCHK(hipMemsetAsync(e->cc_idx, 0, (size_t)ncc * CAPC * sizeof(uint32_t), s));
     HIPCHK(hipMemsetAsync(e->cc_rec, 0, (size_t)ncc * CAPC * sizeof(float4), s));
     HIPCHK(hipMalloc(&e->fc_cnt, (size_t)nc * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->fc_rec, (size_t)nc * CAPF * sizeof(float4)));
-    HIPCHK(hipMalloc(&e->fc_lab, (size_t)nc * CAPF * sizeof(int32_t)));
-    HIPCHK(hipMalloc(&e->fc_slot, (size_t)nc * CAPF));
+    // candidate lists: two parity halves (current / previous iteration)
+    HIPCHK(hipMalloc(&e->fc_rec, (size_t)2 * nc * CAPF * sizeof(float4)));
+    HIPCHK(hipMalloc(&e->fc_lab, (size_t)2 * nc * CAPF * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&e->fc_slot, (size_t)2 * nc * CAPF));
+    HIPCHK(hipMemsetAsync(e->fc_rec, 0, (size_t)2 * nc * CAPF * sizeof(float4), s));
+    HIPCHK(hipMemsetAsync(e->fc_lab, 0, (size_t)2 * nc * CAPF * sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync(e->fc_slot, 0, (size_t)2 * nc * CAPF, s));
     HIPCHK(hipMemsetAsync(e->fc_cnt, 0, (size_t)nc * sizeof(uint32_t), s));
 
     if (n == 0) {
@@ -489,7 +498,8 @@ static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
         const long long fblocks = e->g.ncoarse * ((nchild + FINE_WAVES - 1) / FINE_WAVES);
         k_fine<D><<<(int)fblocks, 64 * FINE_WAVES, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->cc_rec,
                                                            e->fc_cnt, e->fc_rec,
-                                                    e->fc_lab, e->fc_slot, e->tile_off, e->tiles, e->ctrl, gate);
+                                                    e->fc_lab, e->fc_slot, e->tile_off, e->tiles,
+                                                    (long long)e->g.ncells * CAPF, e->ctrl, gate);
         LAUNCHCHK();
         return 0;
     });
@@ -515,12 +525,35 @@ static AssignArgs assign_args(pcm_engine *e) {
     A.fc_lab = e->fc_lab;
     A.fc_slot = e->fc_slot;
     A.C = e->C;
+    A.Cold = e->Cold;
+    A.lstride = (long long)e->g.ncells * CAPF;
+    A.inert_out = &e->ctrl->inertia;
     A.K = e->k;
     for (int a = 0; a < MAXD; ++a) A.q[a] = e->qe.q[a];
     A.lab = e->lab;
     A.partials = e->partials;
     A.ctrl = e->ctrl;
     return A;
+}
+
+// E-step with the current centres: candidate lists, then labels (sorted
+// order, e->lab) and the inertia added into *inert.  Not gated.
+static int launch_labels(pcm_engine *e, hipStream_t s, double *inert) {
+    if (int rc = launch_candidates(e, s, 0)) return rc;
+    AssignArgs A = assign_args(e);
+    A.inert_out = inert;
+    return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        if (e->ntiles == 0) return 0;
+        return dispatch_l(e, [&](auto L) -> int {
+            using LT = decltype(L);
+            k_assign<TT, D, LT, 1><<<assign_grid(e, (const void *)k_assign<TT, D, LT, 1>, 0), TPB, 0, s>>>(
+                A, e->tiles, e->fc_rec, e->fc_lab, e->fc_slot);
+            LAUNCHCHK();
+            return 0;
+        });
+    });
 }
 
 // Fold completed event pairs into the sums (non-blocking unless the ring is full).
@@ -570,7 +603,7 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
         if (e->ntiles > 0) {
-            const size_t lds = (size_t)MSLOT * (D + 1) * TPB * sizeof(uint32_t);
+            const size_t lds = (size_t)AccW<D>::words * sizeof(uint32_t);
             int rc = dispatch_l(e, [&](auto L) -> int {
                 using LT = decltype(L);
                 k_assign<TT, D, LT, 0><<<assign_grid(e, (const void *)k_assign<TT, D, LT, 0>, lds), TPB, lds, s>>>(
@@ -594,7 +627,8 @@ int pcm_iter_global(pcm_engine *e, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_global<D><<<1, 1024, 0, s>>>(e->stats, e->k, e->qe, e->held, e->C, e->Cn, e->hist_changed, e->hist_shift,
+        k_global<D><<<1, 1024, 0, s>>>(e->stats, e->k, e->qe, e->held, e->C, e->Cn, e->Cold, e->hist_changed,
+                                       e->hist_shift,
                                        e->ctrl);
         LAUNCHCHK();
         return timing_mark(e, 3, s);
@@ -661,6 +695,8 @@ int pcm_reloc_candidates(pcm_engine *e, int m, void *records, void *stream) {
             rc = fail(PCM_E_NOMEM, "reloc scratch");
             break;
         }
+        // labels of the halted iteration (the iterations keep no label array)
+        if ((rc = launch_labels(e, s, e->scratch_d))) break;
         rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
             using TT = decltype(T);
             constexpr int D = decltype(DD)::value;
@@ -729,22 +765,7 @@ int pcm_final(pcm_engine *e, void *stream) {
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipMemsetAsync(&e->ctrl->inertia, 0, sizeof(double), s));
-    if (int rc = launch_candidates(e, s, 0)) return rc;
-    AssignArgs A = assign_args(e);
-    return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-        using TT = decltype(T);
-        constexpr int D = decltype(DD)::value;
-        if (e->ntiles > 0) {
-            return dispatch_l(e, [&](auto L) -> int {
-                using LT = decltype(L);
-                k_assign<TT, D, LT, 1><<<assign_grid(e, (const void *)k_assign<TT, D, LT, 1>, 0), TPB, 0, s>>>(
-                    A, e->tiles, e->fc_rec, e->fc_lab, e->fc_slot);
-                LAUNCHCHK();
-                return 0;
-            });
-        }
-        return 0;
-    });
+    return launch_labels(e, s, &e->ctrl->inertia);
 }
 
 int pcm_labels(pcm_engine *e, int32_t *out, void *stream) {

@@ -338,9 +338,10 @@ __global__ __launch_bounds__(256) void k_coarse(Grid g, const float4 *__restrict
 // A cell's candidate count goes to fc_cnt and into the .w of each of its tiles
 // (so the assign kernel reaches its candidates in one dependent load).
 __device__ __forceinline__ void publish_m(long long cell, uint32_t m, uint32_t *fc_cnt, uint32_t o0, uint32_t o1,
-                                           uint4 *tiles) {
+                                          uint4 *tiles, unsigned p) {
     fc_cnt[cell] = m;
-    for (uint32_t o = o0; o < o1; ++o) tiles[o].w = m;
+    const unsigned short m16 = (m == FULL) ? (unsigned short)0xffffu : (unsigned short)m;
+    for (uint32_t o = o0; o < o1; ++o) reinterpret_cast<unsigned short *>(&tiles[o].w)[p] = m16;
 }
 
 // Fine candidate lists: one wave per fine cell, FINE_WAVES cells of the same
@@ -360,8 +361,14 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
                                                           uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
                                                           int32_t *__restrict__ fc_lab, uint8_t *__restrict__ fc_slot,
                                                           const uint32_t *__restrict__ toff, uint4 *__restrict__ tiles,
-                                                          const Ctrl *__restrict__ ctrl, int gate) {
+                                                          long long lstride, const Ctrl *__restrict__ ctrl, int gate) {
     if (gate && gated(ctrl)) return;
+    // lists of iteration `iter` go to parity half iter & 1 (the assign kernel
+    // also reads the previous iteration's half)
+    const unsigned p = ctrl->iter & 1u;
+    fc_rec += (size_t)p * lstride;
+    fc_lab += (size_t)p * lstride;
+    fc_slot += (size_t)p * lstride;
     int nchild = 1;
     for (int a = 0; a < D; ++a) nchild *= g.F;
     const int bpc = (nchild + FINE_WAVES - 1) / FINE_WAVES;      // blocks per coarse cell
@@ -395,7 +402,7 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
     const long long cell = encode(f, g.G, D);
     const uint32_t to0 = toff[cell], to1 = toff[cell + 1];   // issued early, used at the end
     if (!g.prune) {
-        if (lane == 0) publish_m(cell, FULL, fc_cnt, to0, to1, tiles);
+        if (lane == 0) publish_m(cell, FULL, fc_cnt, to0, to1, tiles, p);
         return;
     }
     double blo[MAXD], bhi[MAXD];
@@ -454,7 +461,7 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
         }
         fc_slot[cell * CAPF + lane] = (uint8_t)rank;
     }
-    if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, to0, to1, tiles);
+    if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, to0, to1, tiles, p);
 }
 
 // ------------------------------------------------------------------ assign
@@ -466,6 +473,7 @@ __device__ __forceinline__ void scan4(P rec, int mm, const float (&x)[4][D], flo
         const float4 c = rec[0];
         for (int e = 0; e < 4; ++e) { bd[e] = dist_canon<D>(x[e], c); bj[e] = 0; }
     }
+#pragma unroll 2
     for (int j = 1; j < mm; ++j) {
         const float4 c = rec[j];
         for (int e = 0; e < 4; ++e) {
@@ -480,13 +488,16 @@ __device__ __forceinline__ void scan4(P rec, int mm, const float (&x)[4][D], flo
 struct AssignArgs {
     const void *xs;                 // packed AoS [npad][D] of T, cell order
     long long npad;
-    void *lab;                      // sorted-order labels, LT[npad] (in: previous, out: new)
-    const uint4 *tiles;             // {cell, start, end, m}; m written by k_fine each iteration
+    void *lab;                      // sorted-order labels, LT[npad] (MODE 1 output)
+    const uint4 *tiles;             // {cell, start, end, m0 | m1 << 16}; m_p written by k_fine (parity p)
     long long ntiles;
     const float4 *fc_rec;
     const int32_t *fc_lab;
     const uint8_t *fc_slot;
     const float4 *C;                // all centres (FULL cells)
+    const float4 *Cold;             // previous iteration's centres (FULL cells of the old list)
+    long long lstride;              // ncells * CAPF: distance between the two parity halves of fc_*
+    double *inert_out;              // MODE 1 inertia accumulator
     int K;
     int q[MAXD];
     unsigned long long *partials;   // [NREP][K][D+1]
@@ -535,12 +546,6 @@ __device__ __forceinline__ void load_x(Raw<T, D> &r, rsrc_t rs, unsigned off_pt)
     }
 }
 #define LOAD_X(dst, off) load_x<T, D>(dst, rx, off)
-__device__ __forceinline__ void load_l(RawLab<uint16_t> &r, rsrc_t rs, unsigned off_elem) {
-    r.w = __builtin_amdgcn_raw_buffer_load_b64(rs, off_elem * 2u, 0, 0);
-}
-__device__ __forceinline__ void load_l(RawLab<int32_t> &r, rsrc_t rs, unsigned off_elem) {
-    r.w = __builtin_amdgcn_raw_buffer_load_b128(rs, off_elem * 4u, 0, 0);
-}
 template <int D>
 __device__ __forceinline__ void unpack_x(const Raw<float, D> &r, float (&x)[4][D]) {
     for (int e = 0; e < 4; ++e)
@@ -556,11 +561,6 @@ __device__ __forceinline__ void unpack_x(const Raw<__half, D> &r, float (&x)[4][
             x[e][a] = __half2float(__ushort_as_half(hb));
         }
 }
-__device__ __forceinline__ int lab_at(const RawLab<uint16_t> &r, int e) {
-    const unsigned word = r.w[e >> 1];
-    return (int)((e & 1) ? (word >> 16) : (word & 0xffffu));
-}
-__device__ __forceinline__ int lab_at(const RawLab<int32_t> &r, int e) { return (int)r.w[e]; }
 __device__ __forceinline__ void store_l4(rsrc_t rs, unsigned off, const int (&l)[4], const bool (&v)[4],
                                          RawLab<uint16_t> *) {
     if (v[0] & v[1] & v[2] & v[3]) {
@@ -585,24 +585,40 @@ __device__ __forceinline__ void store_l4(rsrc_t rs, unsigned off, const int (&l)
     }
 }
 
-struct TileH {
-    unsigned cell, start, end, base0;
-    int mm, nr, full, pad_;
+// Per-lane slot accumulators: row-major per thread with an odd stride, so the
+// per-lane atomics (consecutive tids) and the flush reads hit distinct banks.
+template <int D> struct AccW {
+    static constexpr int rows = MSLOT * (D + 1);
+    static constexpr int w = rows | 1;
+    static constexpr int words = TPB * w;
 };
 
-__device__ __forceinline__ TileH make_hdr(const uint4 &t, int K) {
+struct TileH {
+    unsigned cell, start, end, base0;
+    int mm, full;     // current list (parity p): size, or FULL -> all K centres
+    int mo, ofull;    // previous iteration's list (parity p^1)
+    int nr, pad_;
+};
+
+__device__ __forceinline__ TileH make_hdr(const uint4 &t, int K, unsigned p) {
     TileH h;
     h.cell = t.x;
     h.start = t.y;
     h.end = t.z;
+    const unsigned mn = p ? (t.w >> 16) : (t.w & 0xffffu);
+    const unsigned mo = p ? (t.w & 0xffffu) : (t.w >> 16);
 #ifdef PCM_DBG_ALLFULL
     h.full = 1;
+    h.ofull = 1;
 #else
-    h.full = (t.w == FULL) ? 1 : 0;
+    h.full = (mn == 0xffffu) ? 1 : 0;
+    h.ofull = (mo == 0xffffu) ? 1 : 0;
 #endif
-    h.mm = h.full ? K : (int)t.w;
+    h.mm = h.full ? K : (int)mn;
+    h.mo = h.ofull ? K : (int)mo;
     h.base0 = h.start & ~3u;
     h.nr = (int)((h.end - h.base0 + 4 * TPB - 1) / (4 * TPB));
+    h.pad_ = 0;
     return h;
 }
 
@@ -610,23 +626,30 @@ __device__ __forceinline__ TileH make_hdr(const uint4 &t, int K) {
 // blocks walk tiles blockIdx.x, +gridDim.x, ...).  Work item = one round of
 // 4 points per lane (1024 points) of one tile; while item k is computed the
 // loads of item k+1 (next round, or the next tile's first round and candidate
-// record) are in flight in the other register set (ping-pong, no copies).
+// records) are in flight in the other register set (ping-pong, no copies).
 // Buffer loads: 32-bit offsets, out-of-range lanes read zeros (no branches).
-// Per tile: candidates in LDS (scan order = ascending centroid index, so the
+//
+// MODE 0 (Lloyd iteration, gated) streams ONLY the points: no label array is
+// read or written.  The previous iteration's label of a point is recomputed
+// from the previous iteration's candidate list of its cell (double-buffered
+// by iteration parity, exact: the same deterministic scan that produced it),
+// so the change count -- sklearn's strict-convergence test,
+// _kmeans.py:717-723 -- costs compute instead of 4 B/point of HBM traffic.
+// Per tile: both lists in LDS (scan order = ascending centroid index, so the
 // lowest index wins ties), per-lane LDS sums for the MSLOT candidate slots
 // ranked nearest to the cell centre (k_fine), rare other winners via global
 // int64 atomics; at the tile end the slot sums are folded into the global
 // partials while the next tile's candidates are installed (2 barriers/tile).
-// MODE 0: Lloyd iteration (labels, change count, statistics); gated.
-// MODE 1: final E-step (labels + inertia); not gated by `done`.
+// MODE 1: E-step with the current centres writing labels (sorted order) and
+// the inertia into *inert_out; not gated (final E-step, relocation keys).
 template <typename T, int D, typename LT, int MODE>
 __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__restrict__ tiles,
                                                 const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
                                                 const uint8_t *__restrict__ fc_slot) {
     if (MODE == 0 && gated(A.ctrl)) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [MSLOT][D+1][TPB]
-    __shared__ float4 srec[CAPF];
-    __shared__ int32_t slab[CAPF];
+    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [TPB][AccW<D>::w]
+    __shared__ float4 nrec[CAPF], orec[CAPF];
+    __shared__ int32_t nlab[CAPF], olab[CAPF];
     __shared__ uint8_t smap[CAPF];
     __shared__ int32_t sinv[2][CAPF];
     const int tid = threadIdx.x;
@@ -634,74 +657,87 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
     const unsigned nt = (unsigned)A.ntiles;
     unsigned t = blockIdx.x;
     if (t >= nt) return;
+    const unsigned iter = A.ctrl->iter;
+    const unsigned p = iter & 1u;
+    const bool first = (MODE == 0) && (iter == 0u);    // previous labels are all "-1"
+    const float4 *lrec_n = fc_rec + (size_t)p * A.lstride, *lrec_o = fc_rec + (size_t)(p ^ 1u) * A.lstride;
+    const int32_t *llab_n = fc_lab + (size_t)p * A.lstride, *llab_o = fc_lab + (size_t)(p ^ 1u) * A.lstride;
+    const uint8_t *lslot_n = fc_slot + (size_t)p * A.lstride;
     const unsigned cl = tid < CAPF ? (unsigned)tid : (unsigned)(CAPF - 1);   // candidate lane (clamped)
-#ifdef PCM_DBG_VTILES
-    auto tile_at = [&](unsigned i) {
-        const uint4 *p = tiles + (i < nt ? i : nt - 1);
-        uint4 v;
-        v.x = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(&p->x));
-        v.y = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(&p->y));
-        v.z = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(&p->z));
-        v.w = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(&p->w));
-        return v;
-    };
-#else
     auto tile_at = [&](unsigned i) { return tiles[i < nt ? i : nt - 1]; };
-#endif
 
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     const rsrc_t rl = make_rsrc(A.lab, (unsigned long long)A.npad * sizeof(LT));
 
     if (MODE == 0)
-        for (int e = tid; e < MSLOT * (D + 1) * TPB / 4; e += TPB)
-            reinterpret_cast<uint4 *>(acc)[e] = make_uint4(0u, 0u, 0u, 0u);
+        for (int e = tid; e < AccW<D>::words; e += TPB) acc[e] = 0u;
 
     // Pipeline state: h = tile being computed, h1 = next tile (header known),
-    // tl2 = raw record of the tile after that; crec/clab/cslot = h1's candidates.
-    TileH h = make_hdr(tile_at(t), A.K);
-    {
-        const float4 c0 = fc_rec[(size_t)h.cell * CAPF + cl];
-        const int l0 = fc_lab[(size_t)h.cell * CAPF + cl];
-        const int s0 = fc_slot[(size_t)h.cell * CAPF + cl];
-        if (!h.full && tid < h.mm) {
-            srec[tid] = c0;
-            slab[tid] = l0;
-            smap[tid] = (uint8_t)s0;
-            sinv[0][s0] = l0;
+    // tl2 = raw record of the tile after that; c* = h1's candidate records.
+    float4 crec, corec;
+    int clab, colab, cslot;
+    auto fetch = [&](const TileH &hh) {
+        const size_t b = (size_t)hh.cell * CAPF + cl;
+        crec = lrec_n[b];
+        clab = llab_n[b];
+        cslot = lslot_n[b];
+        if (MODE == 0) {
+            corec = lrec_o[b];
+            colab = llab_o[b];
         }
-        if (h.full && tid < MSLOT) sinv[0][tid] = tid;
-    }
-    TileH h1 = make_hdr(tile_at(t + G), A.K);
-    uint4 tl2 = tile_at(t + 2 * G);
-    float4 crec = fc_rec[(size_t)h1.cell * CAPF + cl];
-    int clab = fc_lab[(size_t)h1.cell * CAPF + cl];
-    int cslot = fc_slot[(size_t)h1.cell * CAPF + cl];
+    };
+    auto install = [&](const TileH &hh, int sp) {
+        if (!hh.full && tid < hh.mm) {
+            nrec[tid] = crec;
+            nlab[tid] = clab;
+            smap[tid] = (uint8_t)cslot;
+            sinv[sp][cslot] = clab;
+        }
+        if (hh.full && tid < MSLOT) sinv[sp][tid] = tid;
+        if (MODE == 0 && !hh.ofull && tid < hh.mo) {
+            orec[tid] = corec;
+            olab[tid] = colab;
+        }
+    };
+    TileH h = make_hdr(tile_at(t), A.K, p);
+    fetch(h);
+    install(h, 0);
+    TileH h1 = make_hdr(tile_at(t + G), A.K, p);
+    TileH h2 = make_hdr(tile_at(t + 2 * G), A.K, p);
+    uint4 tl3 = tile_at(t + 3 * G);
+    fetch(h1);
 
-    Raw<T, D> xa, xb;
-    RawLab<LT> la, lb_;
-    LOAD_X(xa, h.base0 + 4u * tid);
-    load_l(la, rl, h.base0 + 4u * tid);
+    int r = 0;
+    // point offset of the work item k rounds ahead of (h, r): in h, h1 or h2
+    // (every tile has >= 1 round, k <= 2); past the last tile: out of range.
+    auto item_off = [&](int k) -> unsigned {
+        int rr = r + k;
+        if (rr < h.nr) return h.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
+        rr -= h.nr;
+        if (t + G >= nt) return 0x0ffffff0u;   // out of range (x D*sizeof(T) bytes): the buffer load returns zeros
+        if (rr < h1.nr) return h1.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
+        rr -= h1.nr;
+        if (t + 2 * G >= nt) return 0x0ffffff0u;
+        return h2.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
+    };
+
+    Raw<T, D> xa, xb, xc;
+    LOAD_X(xa, item_off(0));
+    LOAD_X(xb, item_off(1));
     __syncthreads();
 
     uint32_t nch = 0;
     double inert = 0.0;
     unsigned long long *prep = A.partials + (size_t)(blockIdx.x % NREP) * A.K * (D + 1);
-    int r = 0;
     int par = 0;                       // sinv parity of the current tile
 
-    // One work item (one round of h): prefetch the following item into (nx, nl)
-    // with unconditional loads, compute (cx, cl_), and at the tile's last round
-    // fold its slot sums and install h1's candidates.
-    auto step = [&](Raw<T, D> &cx, RawLab<LT> &clw, Raw<T, D> &nx, RawLab<LT> &nl) -> bool {
+    // One work item (one round of h): prefetch the item two ahead into nx
+    // with unconditional loads (three register sets rotate), compute cx, and
+    // at the tile's last round fold its slot sums and install h1's candidates.
+    auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx) -> bool {
         const bool last_round = (r + 1 == h.nr);
         const bool has_next = (t + G) < nt;
-        unsigned onext = 0x0ffffff0u;   // out of range (x D*sizeof(T) bytes): the buffer load returns zeros
-        if (!last_round)
-            onext = h.base0 + (unsigned)(r + 1) * 4u * TPB + 4u * tid;
-        else if (has_next)
-            onext = h1.base0 + 4u * tid;
-        LOAD_X(nx, onext);
-        load_l(nl, rl, onext);
+        LOAD_X(nx, item_off(2));
 
         const unsigned i0 = h.base0 + (unsigned)r * 4u * TPB + 4u * tid;
         if (i0 < h.end) {
@@ -712,41 +748,59 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
             float bd[4];
             int bj[4];
 #ifdef PCM_ABL_NOCOMPUTE
-            for (int e = 0; e < 4; ++e) { bd[e] = x[e][0]; bj[e] = (x[e][D - 1] > 0.5f) ? 1 : 0; }
-#elif defined(PCM_DBG_GREC)
-            if (h.full)
-                scan4<D>(A.C, h.mm, x, bd, bj);
-            else
-                scan4<D>(fc_rec + (size_t)h.cell * CAPF, h.mm, x, bd, bj);
+            for (int e = 0; e < 4; ++e) { bd[e] = x[e][0]; bj[e] = 0; }
 #else
-            if (h.full)
+            if (MODE == 0 && h.mm == 1) {
+                for (int e = 0; e < 4; ++e) { bd[e] = 0.f; bj[e] = 0; }
+            } else if (h.full) {
                 scan4<D>(A.C, h.mm, x, bd, bj);
-            else
-                scan4<D>(srec, h.mm, x, bd, bj);
+            } else {
+                scan4<D>(nrec, h.mm, x, bd, bj);
+            }
 #endif
             int lbl[4];
-            for (int e = 0; e < 4; ++e) lbl[e] = h.full ? bj[e] : slab[bj[e]];
-            store_l4(rl, i0, lbl, v, (RawLab<LT> *)nullptr);
+            for (int e = 0; e < 4; ++e) lbl[e] = h.full ? bj[e] : nlab[bj[e]];
             if (MODE == 0) {
+                if (first) {
+                    for (int e = 0; e < 4; ++e) nch += v[e] ? 1u : 0u;
+                } else {
+                    float od[4];
+                    int oj[4];
+#ifdef PCM_ABL_NOCOMPUTE
+                    for (int e = 0; e < 4; ++e) oj[e] = 0;
+#else
+                    if (h.mo == 1) {
+                        for (int e = 0; e < 4; ++e) oj[e] = 0;
+                    } else if (h.ofull) {
+                        scan4<D>(A.Cold, h.mo, x, od, oj);
+                    } else {
+                        scan4<D>(orec, h.mo, x, od, oj);
+                    }
+#endif
+                    for (int e = 0; e < 4; ++e) {
+                        const int ol = h.ofull ? oj[e] : olab[oj[e]];
+                        nch += (v[e] && lbl[e] != ol) ? 1u : 0u;
+                    }
+                }
                 for (int e = 0; e < 4; ++e) {
                     if (!v[e]) continue;
-                    nch += (lbl[e] != lab_at(clw, e)) ? 1u : 0u;
 #if defined(PCM_ABL_NOACC) || defined(PCM_ABL_NOCOMPUTE)
                     continue;
 #endif
                     const int sl = h.full ? bj[e] : (int)smap[bj[e]];
                     if (sl < MSLOT) {
-                        for (int a = 0; a < D; ++a)
-                            atomicAdd(&acc[(sl * (D + 1) + a) * TPB + tid], (uint32_t)fixed_i(x[e][a], A.q[a]));
-                        atomicAdd(&acc[(sl * (D + 1) + D) * TPB + tid], 1u);
+                        uint32_t *ap = &acc[tid * AccW<D>::w + sl * (D + 1)];
+                        for (int a = 0; a < D; ++a) atomicAdd(ap + a, (uint32_t)fixed_i(x[e][a], A.q[a]));
+                        atomicAdd(ap + D, 1u);
                     } else {
-                        unsigned long long *p = prep + (size_t)lbl[e] * (D + 1);
+                        unsigned long long *pp = prep + (size_t)lbl[e] * (D + 1);
                         for (int a = 0; a < D; ++a)
-                            atomicAdd(p + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
-                        atomicAdd(p + D, 1ull);
+                            atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                        atomicAdd(pp + D, 1ull);
                     }
                 }
             } else {
+                store_l4(rl, i0, lbl, v, (RawLab<LT> *)nullptr);
                 for (int e = 0; e < 4; ++e)
                     if (v[e]) inert += (double)bd[e];
             }
@@ -764,64 +818,54 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
             const int nslots = h.mm < MSLOT ? h.mm : MSLOT;
 #endif
             const int npairs = nslots * (D + 1);
-            for (int p0 = 0; p0 < npairs; p0 += TPB / 8) {
-                const int p = p0 + tid / 8, sub = tid & 7;
+            // 16 threads per row, each summing 16 lanes' words (stride AccW::w: conflict-free)
+            for (int p0 = 0; p0 < npairs; p0 += TPB / 16) {
+                const int pi = p0 + tid / 16, sub = tid & 15;
                 long long sacc = 0;
-                if (p < npairs)
-                    for (int k = 0; k < TPB / 8; ++k) {
-                        uint32_t *ap = &acc[p * TPB + sub + 8 * k];
+                if (pi < npairs) {
+                    const bool cnt = (pi % (D + 1) == D);
+                    for (int k = 0; k < TPB / 16; ++k) {
+                        uint32_t *ap = &acc[(sub + 16 * k) * AccW<D>::w + pi];
                         // per-lane sums are exact int32 (<= 63 points of |xq| < 2^25)
-                        sacc += (p % (D + 1) == D) ? (long long)*ap : (long long)(int32_t)*ap;
+                        sacc += cnt ? (long long)*ap : (long long)(int32_t)*ap;
                         *ap = 0u;
                     }
-                sacc += __shfl_down(sacc, 4, 8);
-                sacc += __shfl_down(sacc, 2, 8);
-                sacc += __shfl_down(sacc, 1, 8);
-                if (p < npairs && sub == 0 && sacc) {
-                    const int slot = p / (D + 1), qq = p % (D + 1);
+                }
+                sacc += __shfl_down(sacc, 8, 16);
+                sacc += __shfl_down(sacc, 4, 16);
+                sacc += __shfl_down(sacc, 2, 16);
+                sacc += __shfl_down(sacc, 1, 16);
+                if (pi < npairs && sub == 0 && sacc) {
+                    const int slot = pi / (D + 1), qq = pi % (D + 1);
                     atomicAdd(prep + (size_t)sinv[par][slot] * (D + 1) + qq, (unsigned long long)sacc);
                 }
             }
         }
         if (!has_next) return false;
-        if (!h1.full && tid < h1.mm) {
-            srec[tid] = crec;
-            slab[tid] = clab;
-            smap[tid] = (uint8_t)cslot;
-            sinv[par ^ 1][cslot] = clab;
-        }
-        if (h1.full && tid < MSLOT) sinv[par ^ 1][tid] = tid;
+        install(h1, par ^ 1);
         par ^= 1;
         h = h1;
+        h1 = h2;
         t += G;
         r = 0;
-        h1 = make_hdr(tl2, A.K);
-        tl2 = tile_at(t + 2 * G);
-        crec = fc_rec[(size_t)h1.cell * CAPF + cl];
-        clab = fc_lab[(size_t)h1.cell * CAPF + cl];
-        cslot = fc_slot[(size_t)h1.cell * CAPF + cl];
+        h2 = make_hdr(tl3, A.K, p);
+        tl3 = tile_at(t + 3 * G);
+        fetch(h1);
         __syncthreads();
         return true;
     };
-#ifdef PCM_DBG_NO_PINGPONG
     while (true) {
-        if (!step(xa, la, xb, lb_)) break;
-        xa = xb;
-        la = lb_;
+        if (!step(xa, xc)) break;
+        if (!step(xb, xa)) break;
+        if (!step(xc, xb)) break;
     }
-#else
-    while (true) {
-        if (!step(xa, la, xb, lb_)) break;
-        if (!step(xb, lb_, xa, la)) break;
-    }
-#endif
 
     if (MODE == 0) {
         for (int o = 32; o > 0; o >>= 1) nch += __shfl_xor(nch, o);
         if ((tid & 63) == 0 && nch) atomicAdd(&A.ctrl->changed_local, (unsigned long long)nch);
     } else {
         for (int o = 32; o > 0; o >>= 1) inert += __shfl_xor(inert, o);
-        if ((tid & 63) == 0) atomicAdd(&A.ctrl->inertia, inert);
+        if ((tid & 63) == 0) atomicAdd(A.inert_out, inert);
     }
 }
 
@@ -853,6 +897,7 @@ template <int D>
 __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__restrict__ stats, int K, QExp qe,
                                                  unsigned long long *__restrict__ held,
                                                  float4 *__restrict__ C, float4 *__restrict__ Cn,
+                                                 float4 *__restrict__ Cold,
                                                  unsigned long long *__restrict__ hist_changed,
                                                  double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl) {
     if (gated(ctrl)) return;
@@ -937,7 +982,10 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
         if (tid < s) ssum[tid] = ssum[tid] + ssum[tid + s];
         __syncthreads();
     }
-    for (int j = tid; j < K; j += 1024) C[j] = Cn[j];
+    for (int j = tid; j < K; j += 1024) {
+        Cold[j] = C[j];
+        C[j] = Cn[j];
+    }
     if (tid == 0) {
         const unsigned long long changed = stats[(size_t)K * (D + 1)];
         const double shift = ssum[0];

@@ -159,7 +159,8 @@ def main():
 
     if rank == 0:
         n_local = hi_row - lo_row
-        bytes_pt = D * 4 + 4
+        # the iteration kernel streams only the points (labels are recomputed, not stored)
+        bytes_pt = D * 4
         achieved = bytes_pt * n_local / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0
         value = N * args.steps / dt
         out = {

@@ -202,3 +202,13 @@ def test_plugin_gpu_matches_oracle(pcm):
     ref = R.lloyd_fit(X, C0, max_iter=30, fast=True)
     np.testing.assert_array_equal(fused[1][1]["properties"]["cluster"], ref["labels"])
     np.testing.assert_array_equal(fused[0][0].astype(np.float32), ref["centers"])
+
+
+def test_unpruned_full_lists(pcm):
+    """Extent >= 1e18 disables pruning: every cell scans all K centres (the
+    FULL path, including the previous-iteration scan over the kept centres)."""
+    X = (R.splitmix_uniform(6000, 3, 31).astype(np.float64) * 4e18 - 2e18).astype(np.float32)
+    C0 = X[R.init_indices(6000, 24)]
+    ref = R.lloyd_fit(X, C0, max_iter=25, tol=0.0, fast=True)
+    res = gpu_fit(pcm, X, C0, 25)
+    assert_same(res, ref, "unpruned")

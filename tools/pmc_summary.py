@@ -1,36 +1,47 @@
-"""Summarise rocprofv3 --pmc CSVs for one kernel: mean per dispatch over the
-last dispatches (skips warm-up), plus derived HBM traffic.
+"""Summarise rocprofv3 --pmc output (rocpd .db or *counter_collection.csv) for
+one kernel: mean per dispatch over the dispatches after the first (warm-up).
 
-gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads half the bytes
-of a wide (16 B/lane) coalesced streaming read -> x2; WRITE_SIZE is exact for
-16 B/lane stores (our label stores are 8 B/lane: uncalibrated, reported as is).
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half
+the bytes of a wide (16 B/lane) coalesced streaming read -> x2.
+usage: python tools/pmc_summary.py KERNEL_SUBSTR DIR [DIR ...]
 """
 import csv
 import glob
 import json
+import sqlite3
 import sys
 from collections import defaultdict
 
 
-def load(paths, kernel):
-    per = defaultdict(dict)
+def load_db(path, kernel):
+    per = defaultdict(lambda: defaultdict(float))
+    c = sqlite3.connect(path)
+    q = "select dispatch_id, counter_name, value, start, end from counters_collection where kernel_name like ?"
+    for did, name, val, st, en in c.execute(q, (f"%{kernel}%",)):
+        per[did][name] += float(val)
+        per[did]["_ns"] = en - st
+    return per
+
+
+def load_csv(paths, kernel):
+    per = defaultdict(lambda: defaultdict(float))
     for p in paths:
         for r in csv.DictReader(open(p)):
             if kernel in r["Kernel_Name"]:
-                per[int(r["Dispatch_Id"])][r["Counter_Name"]] = per[int(r["Dispatch_Id"])].get(
-                    r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-                per[int(r["Dispatch_Id"])]["_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                d = int(r["Dispatch_Id"])
+                per[d][r["Counter_Name"]] += float(r["Counter_Value"])
+                per[d]["_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     return per
 
 
 def main():
-    kernel = sys.argv[1]
-    dirs = sys.argv[2:]
+    kernel, dirs = sys.argv[1], sys.argv[2:]
     agg = defaultdict(list)
     for d in dirs:
-        per = load(glob.glob(f"{d}/*counter_collection.csv"), kernel)
-        ids = sorted(per)[1:]            # drop the first (warm-up) dispatch
-        for i in ids:
+        dbs = glob.glob(f"{d}/**/*.db", recursive=True)
+        per = load_db(dbs[0], kernel) if dbs else load_csv(glob.glob(f"{d}/**/*counter_collection.csv",
+                                                                      recursive=True), kernel)
+        for i in sorted(per)[1:]:
             for k, v in per[i].items():
                 agg[k].append(v)
     out = {k: sum(v) / len(v) for k, v in agg.items()}
@@ -38,7 +49,7 @@ def main():
         out["hbm_read_bytes_corrected"] = out["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in out:
         out["hbm_write_bytes"] = out["WRITE_SIZE"] * 1024
-    print(json.dumps(out, indent=1))
+    print(json.dumps(out, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":

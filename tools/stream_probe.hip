@@ -1,0 +1,108 @@
+// Calibration only: the HBM ceiling of the assign kernel's access mix
+// (read 12 B/pt AoS fp32 + read 2 B/pt u16 label + write 2 B/pt label) with
+// no compute, as plain streaming kernels.  Build: hipcc --offload-arch=gfx950 -O3
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t mk(const void *p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)p, (short)0, (int)bytes, 0x00020000);
+}
+
+// one block per 1024-point chunk, 4 points per lane
+template <int WRITE>
+__global__ __launch_bounds__(256) void k_chunk(const float *xs, unsigned short *lab, unsigned n, unsigned *sink) {
+    const rsrc_t rx = mk(xs, n * 12u), rl = mk(lab, n * 2u);
+    const unsigned p = blockIdx.x * 1024u + 4u * threadIdx.x;
+    u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u, 0, 0);
+    u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u + 16u, 0, 0);
+    u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u + 32u, 0, 0);
+    u32x2 l = __builtin_amdgcn_raw_buffer_load_b64(rl, p * 2u, 0, 0);
+    unsigned v = a[0] ^ a[3] ^ b[2] ^ c[1];
+    u32x2 w;
+    w[0] = ((a[0] >> 31) | ((a[3] >> 31) << 16)) ^ (l[0] & 0x10001u);
+    w[1] = ((b[2] >> 31) | ((c[1] >> 31) << 16)) ^ (l[1] & 0x10001u);
+    if (WRITE) __builtin_amdgcn_raw_buffer_store_b64(w, rl, p * 2u, 0, 0);
+    else if (v == 0x12345678u) sink[0] = w[0] ^ w[1];
+}
+
+// persistent: G blocks stride over chunks, two chunks in flight (ping-pong)
+template <int WRITE>
+__global__ __launch_bounds__(256) void k_persist(const float *xs, unsigned short *lab, unsigned n, unsigned nchunk,
+                                                 unsigned *sink) {
+    const rsrc_t rx = mk(xs, n * 12u), rl = mk(lab, n * 2u);
+    unsigned acc = 0;
+    unsigned ch = blockIdx.x;
+    u32x4 a[2], b[2], c[2];
+    u32x2 l[2];
+    auto ld = [&](int s, unsigned chunk) {
+        const unsigned p = chunk < nchunk ? chunk * 1024u + 4u * threadIdx.x : 0x0ffffff0u;
+        a[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u, 0, 0);
+        b[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u + 16u, 0, 0);
+        c[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u + 32u, 0, 0);
+        l[s] = __builtin_amdgcn_raw_buffer_load_b64(rl, p * 2u, 0, 0);
+    };
+    auto use = [&](int s, unsigned chunk) {
+        const unsigned p = chunk * 1024u + 4u * threadIdx.x;
+        u32x2 w;
+        w[0] = ((a[s][0] >> 31) | ((a[s][3] >> 31) << 16)) ^ (l[s][0] & 0x10001u);
+        w[1] = ((b[s][2] >> 31) | ((c[s][1] >> 31) << 16)) ^ (l[s][1] & 0x10001u);
+        if (WRITE) __builtin_amdgcn_raw_buffer_store_b64(w, rl, p * 2u, 0, 0);
+        acc ^= w[0] ^ w[1] ^ a[s][1] ^ b[s][1] ^ c[s][3];
+    };
+    ld(0, ch);
+    while (true) {
+        ld(1, ch + gridDim.x);
+        use(0, ch);
+        ch += gridDim.x;
+        if (ch >= nchunk) break;
+        ld(0, ch + gridDim.x);
+        use(1, ch);
+        ch += gridDim.x;
+        if (ch >= nchunk) break;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+int main(int argc, char **argv) {
+    const unsigned n = 100000000u / 1024u * 1024u;
+    const unsigned nchunk = n / 1024u;
+    float *xs;
+    unsigned short *lab;
+    unsigned *sink;
+    hipMalloc(&xs, (size_t)n * 12);
+    hipMalloc(&lab, (size_t)n * 2);
+    hipMalloc(&sink, 64);
+    hipMemset(xs, 0x3f, (size_t)n * 12);
+    hipMemset(lab, 0, (size_t)n * 2);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto run = [&](const char *name, double bytes, auto launch) {
+        for (int i = 0; i < 3; ++i) launch();
+        hipEventRecord(e0);
+        const int R = 20;
+        for (int i = 0; i < R; ++i) launch();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        ms /= R;
+        printf("%-28s %8.1f us  %7.0f GB/s\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+    };
+    const double rw = (double)n * 16, ro = (double)n * 14;
+    run("chunk r+w (16B/pt)", rw, [&] { k_chunk<1><<<nchunk, 256>>>(xs, lab, n, sink); });
+    run("chunk read (14B/pt)", ro, [&] { k_chunk<0><<<nchunk, 256>>>(xs, lab, n, sink); });
+    for (int bpc : {2, 4, 8, 16}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "persist r+w %d/CU", bpc);
+        run(nm, rw, [&] { k_persist<1><<<256 * bpc, 256>>>(xs, lab, n, nchunk, sink); });
+        snprintf(nm, sizeof nm, "persist read %d/CU", bpc);
+        run(nm, ro, [&] { k_persist<0><<<256 * bpc, 256>>>(xs, lab, n, nchunk, sink); });
+    }
+    return 0;
+}
