@@ -58,8 +58,8 @@ struct pcm_engine {
     float4 *cc_rec = nullptr;
     float4 *fc_rec = nullptr;
     int32_t *fc_lab = nullptr;
-    uint8_t *fc_slot = nullptr;
-    float4 *C = nullptr, *Cn = nullptr, *Cold = nullptr;
+    float4 *C = nullptr, *Cn = nullptr;
+    unsigned long long *prev = nullptr;        // raw statistics of the previous iteration
     double *scratch_d = nullptr;
     unsigned long long *partials = nullptr, *stats = nullptr, *hist_changed = nullptr;
     unsigned long long *stats_own = nullptr;   // engine-owned; `stats` may point at a bound buffer
@@ -132,12 +132,11 @@ int dispatch_l(const pcm_engine *e, F &&f) {
 
 void free_layout(pcm_engine *e) {
     void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->cc_cnt, e->cc_idx,
-                  e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->fc_slot, e->cc_rec};
+                  e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->cc_rec};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
     e->tile_off = nullptr;
-    e->fc_slot = nullptr;
     e->cc_rec = nullptr;
     e->cc_cnt = nullptr; e->cc_idx = nullptr; e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
     e->layout_ready = false;
@@ -240,8 +239,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     hipError_t err = hipSuccess;
     err = err ? err : hipMalloc(&e->C, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
-    err = err ? err : hipMalloc(&e->Cold, (size_t)k * sizeof(float4));
-    err = err ? err : hipMemset(e->Cold, 0, (size_t)k * sizeof(float4));
+    err = err ? err : hipMalloc(&e->prev, nstat * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->scratch_d, sizeof(double));
     err = err ? err : hipMalloc(&e->partials, (size_t)NREP * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
@@ -271,7 +269,7 @@ int pcm_engine_destroy(pcm_engine *e) {
         for (int j = 0; j < 4; ++j)
             if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
     free_layout(e);
-    void *ps[] = {e->C, e->Cn, e->Cold, e->scratch_d, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
+    void *ps[] = {e->C, e->Cn, e->prev, e->scratch_d, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
                   e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx};
     for (void *p : ps)
         if (p) (void)hipFree(p);
@@ -349,10 +347,8 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     // candidate lists: two parity halves (current / previous iteration)
     HIPCHK(hipMalloc(&e->fc_rec, (size_t)2 * nc * CAPF * sizeof(float4)));
     HIPCHK(hipMalloc(&e->fc_lab, (size_t)2 * nc * CAPF * sizeof(int32_t)));
-    HIPCHK(hipMalloc(&e->fc_slot, (size_t)2 * nc * CAPF));
     HIPCHK(hipMemsetAsync(e->fc_rec, 0, (size_t)2 * nc * CAPF * sizeof(float4), s));
     HIPCHK(hipMemsetAsync(e->fc_lab, 0, (size_t)2 * nc * CAPF * sizeof(int32_t), s));
-    HIPCHK(hipMemsetAsync(e->fc_slot, 0, (size_t)2 * nc * CAPF, s));
     HIPCHK(hipMemsetAsync(e->fc_cnt, 0, (size_t)nc * sizeof(uint32_t), s));
 
     if (n == 0) {
@@ -476,6 +472,9 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
     });
     if (rc) return rc;
     HIPCHK(hipMemsetAsync(e->lab, 0xff, (size_t)e->npad * lsize(e), s));   // "no label yet" (-1 / 0xffff)
+    // previous raw statistics := 0: iteration 0 "converges" only for an empty cloud,
+    // as sklearn's labels-vs-(-1) comparison does
+    HIPCHK(hipMemsetAsync(e->prev, 0, ((size_t)e->k * (e->d + 1) + 1) * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->partials, 0, (size_t)NREP * e->k * (e->d + 1) * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->hist_changed, 0, (size_t)e->max_iter_cap * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->hist_shift, 0, (size_t)e->max_iter_cap * sizeof(double), s));
@@ -498,7 +497,7 @@ static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
         const long long fblocks = e->g.ncoarse * ((nchild + FINE_WAVES - 1) / FINE_WAVES);
         k_fine<D><<<(int)fblocks, 64 * FINE_WAVES, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->cc_rec,
                                                            e->fc_cnt, e->fc_rec,
-                                                    e->fc_lab, e->fc_slot, e->tile_off, e->tiles,
+                                                    e->fc_lab, e->tile_off, e->tiles,
                                                     (long long)e->g.ncells * CAPF, e->ctrl, gate);
         LAUNCHCHK();
         return 0;
@@ -515,22 +514,18 @@ static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
     return (int)std::min<long long>(e->ntiles, (long long)per_cu * e->num_cu);
 }
 
-static AssignArgs assign_args(pcm_engine *e) {
-    AssignArgs A{};
+static LloydArgs lloyd_args(pcm_engine *e) {
+    LloydArgs A{};
     A.xs = e->xs;
     A.npad = e->npad;
     A.tiles = e->tiles;
     A.ntiles = e->ntiles;
     A.fc_rec = e->fc_rec;
     A.fc_lab = e->fc_lab;
-    A.fc_slot = e->fc_slot;
     A.C = e->C;
-    A.Cold = e->Cold;
     A.lstride = (long long)e->g.ncells * CAPF;
-    A.inert_out = &e->ctrl->inertia;
     A.K = e->k;
     for (int a = 0; a < MAXD; ++a) A.q[a] = e->qe.q[a];
-    A.lab = e->lab;
     A.partials = e->partials;
     A.ctrl = e->ctrl;
     return A;
@@ -540,16 +535,14 @@ static AssignArgs assign_args(pcm_engine *e) {
 // order, e->lab) and the inertia added into *inert.  Not gated.
 static int launch_labels(pcm_engine *e, hipStream_t s, double *inert) {
     if (int rc = launch_candidates(e, s, 0)) return rc;
-    AssignArgs A = assign_args(e);
-    A.inert_out = inert;
+    LloydArgs A = lloyd_args(e);
     return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
         if (e->ntiles == 0) return 0;
         return dispatch_l(e, [&](auto L) -> int {
             using LT = decltype(L);
-            k_assign<TT, D, LT, 1><<<assign_grid(e, (const void *)k_assign<TT, D, LT, 1>, 0), TPB, 0, s>>>(
-                A, e->tiles, e->fc_rec, e->fc_lab, e->fc_slot);
+            k_label<TT, D, LT><<<assign_grid(e, (const void *)k_label<TT, D, LT>, 0), TPB, 0, s>>>(A, e->lab, inert);
             LAUNCHCHK();
             return 0;
         });
@@ -598,20 +591,14 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
     if (int rc = timing_mark(e, 0, s)) return rc;
     if (int rc = launch_candidates(e, s, 1)) return rc;
     if (int rc = timing_mark(e, 1, s)) return rc;
-    AssignArgs A = assign_args(e);
+    LloydArgs A = lloyd_args(e);
     return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
         if (e->ntiles > 0) {
-            const size_t lds = (size_t)AccW<D>::words * sizeof(uint32_t);
-            int rc = dispatch_l(e, [&](auto L) -> int {
-                using LT = decltype(L);
-                k_assign<TT, D, LT, 0><<<assign_grid(e, (const void *)k_assign<TT, D, LT, 0>, lds), TPB, lds, s>>>(
-                    A, e->tiles, e->fc_rec, e->fc_lab, e->fc_slot);
-                LAUNCHCHK();
-                return 0;
-            });
-            if (rc) return rc;
+            const size_t lds = (size_t)AccL<D>::words * sizeof(uint32_t);
+            k_lloyd<TT, D><<<assign_grid(e, (const void *)k_lloyd<TT, D>, lds), TPB, lds, s>>>(A);
+            LAUNCHCHK();
         }
         if (int rc = timing_mark(e, 2, s)) return rc;
         const int nf = e->k * (D + 1) + 1;
@@ -627,7 +614,7 @@ int pcm_iter_global(pcm_engine *e, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_global<D><<<1, 1024, 0, s>>>(e->stats, e->k, e->qe, e->held, e->C, e->Cn, e->Cold, e->hist_changed,
+        k_global<D><<<1, 1024, 0, s>>>(e->stats, e->k, e->qe, e->held, e->prev, e->C, e->Cn, e->hist_changed,
                                        e->hist_shift,
                                        e->ctrl);
         LAUNCHCHK();

@@ -2,8 +2,9 @@
 //
 // Hot path: per iteration
 //   k_coarse / k_fine  exact candidate lists per grid cell (fp64 bisector bound)
-//   k_assign           nearest centroid over the cell's candidates + LDS-privatised
+//   k_lloyd            nearest centroid over the cell's candidates + LDS-privatised
 //                      fixed-point accumulation (replaces _k_means_lloyd.pyx:168-218)
+//   k_label            final E-step: labels + inertia (_kmeans.py:736-750)
 //   k_fold             replica fold of the partials (replaces the locked reduction
 //                      of _k_means_lloyd.pyx:142-152)
 //   k_global           averaging / shift / convergence (_k_means_common.pyx:274-311,
@@ -51,7 +52,7 @@ struct Ctrl {
     uint32_t n_empty, resume, status, pad0;
     double tol;
     double inertia;
-    unsigned long long changed_local;
+    unsigned long long neq_saved;   // stat words changed at a halted iteration (used on resume)
     unsigned long long last_changed;
     double last_shift;
 };
@@ -348,9 +349,7 @@ __device__ __forceinline__ void publish_m(long long cell, uint32_t m, uint32_t *
 // coarse parent per block (the parent list is staged in LDS once per block).
 // Reference r = the parent candidate nearest the cell centre (any centroid is
 // a valid reference; only the pruning test needs the fp64 margins).  Kept
-// candidates stay in ascending centroid order; each also gets its rank by
-// distance to the cell centre (slot 0 = nearest) for the assign kernel's
-// LDS-privatised sums.
+// candidates stay in ascending centroid order (the scan's tie rule).
 constexpr int FINE_WAVES = 4;
 
 template <int D>
@@ -359,16 +358,14 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
                                                           const uint32_t *__restrict__ cc_idx,
                                                           const float4 *__restrict__ cc_rec,
                                                           uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                                          int32_t *__restrict__ fc_lab, uint8_t *__restrict__ fc_slot,
+                                                          int32_t *__restrict__ fc_lab,
                                                           const uint32_t *__restrict__ toff, uint4 *__restrict__ tiles,
                                                           long long lstride, const Ctrl *__restrict__ ctrl, int gate) {
     if (gate && gated(ctrl)) return;
-    // lists of iteration `iter` go to parity half iter & 1 (the assign kernel
-    // also reads the previous iteration's half)
+    // lists of iteration `iter` go to parity half iter & 1
     const unsigned p = ctrl->iter & 1u;
     fc_rec += (size_t)p * lstride;
     fc_lab += (size_t)p * lstride;
-    fc_slot += (size_t)p * lstride;
     int nchild = 1;
     for (int a = 0; a < D; ++a) nchild *= g.F;
     const int bpc = (nchild + FINE_WAVES - 1) / FINE_WAVES;      // blocks per coarse cell
@@ -377,7 +374,6 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     __shared__ float4 prec[CAPC];
     __shared__ int pidx[CAPC];
-    __shared__ float cdist[FINE_WAVES][CAPF];
     int ci[MAXD];
     decode(I, g.GC, D, ci);
     uint32_t mp = cc_cnt[I];
@@ -443,23 +439,8 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *
         if (keep && pos < (uint32_t)CAPF) {
             fc_rec[cell * CAPF + pos] = c;
             fc_lab[cell * CAPF + pos] = j;
-            float cd = 0.f;
-            for (int a = 0; a < D; ++a) {
-                const float dd = ctr[a] - comp(c, a);
-                cd += dd * dd;
-            }
-            cdist[wv][pos] = cd;
         }
         total += __popcll(bal);
-    }
-    if (total <= (uint32_t)CAPF && (uint32_t)lane < total) {
-        const float mine = cdist[wv][lane];
-        uint32_t rank = 0;
-        for (uint32_t o = 0; o < total; ++o) {
-            const float other = cdist[wv][o];
-            rank += (other < mine || (other == mine && o < (uint32_t)lane)) ? 1u : 0u;
-        }
-        fc_slot[cell * CAPF + lane] = (uint8_t)rank;
     }
     if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, to0, to1, tiles, p);
 }
@@ -484,25 +465,6 @@ __device__ __forceinline__ void scan4(P rec, int mm, const float (&x)[4][D], flo
         }
     }
 }
-
-struct AssignArgs {
-    const void *xs;                 // packed AoS [npad][D] of T, cell order
-    long long npad;
-    void *lab;                      // sorted-order labels, LT[npad] (MODE 1 output)
-    const uint4 *tiles;             // {cell, start, end, m0 | m1 << 16}; m_p written by k_fine (parity p)
-    long long ntiles;
-    const float4 *fc_rec;
-    const int32_t *fc_lab;
-    const uint8_t *fc_slot;
-    const float4 *C;                // all centres (FULL cells)
-    const float4 *Cold;             // previous iteration's centres (FULL cells of the old list)
-    long long lstride;              // ncells * CAPF: distance between the two parity halves of fc_*
-    double *inert_out;              // MODE 1 inertia accumulator
-    int K;
-    int q[MAXD];
-    unsigned long long *partials;   // [NREP][K][D+1]
-    Ctrl *ctrl;
-};
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -585,136 +547,165 @@ __device__ __forceinline__ void store_l4(rsrc_t rs, unsigned off, const int (&l)
     }
 }
 
-// Per-lane slot accumulators: row-major per thread with an odd stride, so the
-// per-lane atomics (consecutive tids) and the flush reads hit distinct banks.
-template <int D> struct AccW {
-    static constexpr int rows = MSLOT * (D + 1);
+constexpr int LSLOT = 8;
+
+template <int D> struct AccL {
+    static constexpr int rows = (LSLOT + 1) * (D + 1);   // + junk slot
     static constexpr int w = rows | 1;
     static constexpr int words = TPB * w;
 };
 
-struct TileH {
-    unsigned cell, start, end, base0;
-    int mm, full;     // current list (parity p): size, or FULL -> all K centres
-    int mo, ofull;    // previous iteration's list (parity p^1)
-    int nr, pad_;
+struct LloydArgs {
+    const void *xs;                 // packed AoS [npad][D] of T, cell order
+    long long npad;
+    const uint4 *tiles;             // {cell, start, end, m0 | m1 << 16}; m_p written by k_fine (parity p)
+    long long ntiles;
+    const float4 *fc_rec;
+    const int32_t *fc_lab;
+    const float4 *C;                // all centres (FULL cells)
+    long long lstride;              // distance between the two parity halves of fc_*
+    int K;
+    int q[MAXD];
+    unsigned long long *partials;   // [NREP][K][D+1]
+    const Ctrl *ctrl;
 };
 
-__device__ __forceinline__ TileH make_hdr(const uint4 &t, int K, unsigned p) {
-    TileH h;
+struct TileL {
+    unsigned cell, start, end, base0;
+    int mm, full, nr, pad_;
+};
+
+__device__ __forceinline__ TileL make_tile(const uint4 &t, int K, unsigned p) {
+    TileL h;
     h.cell = t.x;
     h.start = t.y;
     h.end = t.z;
     const unsigned mn = p ? (t.w >> 16) : (t.w & 0xffffu);
-    const unsigned mo = p ? (t.w & 0xffffu) : (t.w >> 16);
-#ifdef PCM_DBG_ALLFULL
-    h.full = 1;
-    h.ofull = 1;
-#else
     h.full = (mn == 0xffffu) ? 1 : 0;
-    h.ofull = (mo == 0xffffu) ? 1 : 0;
-#endif
     h.mm = h.full ? K : (int)mn;
-    h.mo = h.ofull ? K : (int)mo;
     h.base0 = h.start & ~3u;
     h.nr = (int)((h.end - h.base0 + 4 * TPB - 1) / (4 * TPB));
     h.pad_ = 0;
     return h;
 }
 
-// Persistent, software-pipelined assignment (one 256-thread block per slot,
-// blocks walk tiles blockIdx.x, +gridDim.x, ...).  Work item = one round of
-// 4 points per lane (1024 points) of one tile; while item k is computed the
-// loads of item k+1 (next round, or the next tile's first round and candidate
-// records) are in flight in the other register set (ping-pong, no copies).
-// Buffer loads: 32-bit offsets, out-of-range lanes read zeros (no branches).
+// E-step with the current centres writing labels (sorted order) and the
+// inertia (final E-step of _kmeans.py:736-750, relocation keys).  Not gated.
+// Same tile walk and candidate lists as k_lloyd; 4 points per lane per round,
+// the loads of the next round in flight while one is computed.
+template <typename T, int D, typename LT>
+__global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, double *inert_out) {
+    __shared__ float4 crec[CAPF];
+    __shared__ int32_t cid[CAPF];
+    const int tid = threadIdx.x;
+    const unsigned G = gridDim.x;
+    const unsigned nt = (unsigned)A.ntiles;
+    const unsigned p = A.ctrl->iter & 1u;
+    const float4 *lrec = A.fc_rec + (size_t)p * A.lstride;
+    const int32_t *llab = A.fc_lab + (size_t)p * A.lstride;
+    const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
+    const rsrc_t rl = make_rsrc(lab, (unsigned long long)A.npad * sizeof(LT));
+    double inert = 0.0;
+    for (unsigned t = blockIdx.x; t < nt; t += G) {
+        const TileL h = make_tile(A.tiles[t], A.K, p);
+        __syncthreads();
+        if (!h.full && tid < h.mm) {
+            crec[tid] = lrec[(size_t)h.cell * CAPF + tid];
+            cid[tid] = llab[(size_t)h.cell * CAPF + tid];
+        }
+        __syncthreads();
+        Raw<T, D> cur, nxt;
+        LOAD_X(cur, h.base0 + 4u * tid);
+        for (int r = 0; r < h.nr; ++r) {
+            const unsigned i0 = h.base0 + (unsigned)r * 4u * TPB + 4u * tid;
+            LOAD_X(nxt, r + 1 < h.nr ? i0 + 4u * TPB : 0x0ffffff0u);
+            float x[4][D];
+            unpack_x<D>(cur, x);
+            float bd[4];
+            int bj[4];
+            if (h.full) scan4<D>(A.C, h.mm, x, bd, bj);
+            else scan4<D>(crec, h.mm, x, bd, bj);
+            int lbl[4];
+            bool v[4];
+            for (int e = 0; e < 4; ++e) {
+                lbl[e] = h.full ? bj[e] : cid[bj[e]];
+                v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
+                if (v[e]) inert += (double)bd[e];
+            }
+            if (i0 < h.end) store_l4(rl, i0, lbl, v, (RawLab<LT> *)nullptr);
+            cur = nxt;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) inert += __shfl_xor(inert, o);
+    if ((tid & 63) == 0) atomicAdd(inert_out, inert);
+}
+
+// ------------------------------------------------------------------ Lloyd iteration
+// One Lloyd iteration's E-step + accumulation (sklearn's lloyd_iter_chunked_dense
+// with update_centers=True, _k_means_lloyd.pyx:23-165).  It streams ONLY the
+// points (12 B/pt at fp32 D=3): no label array is read or written.  sklearn's
+// strict-convergence test (labels equal, _kmeans.py:717-723) is replaced by
+// "the raw integer statistics equal the previous iteration's" in k_global: equal
+// labels give equal statistics, and equal statistics give equal centres, i.e.
+// shift 0 <= tol, so sklearn stops at that same iteration either way (DESIGN.md
+// "Convergence").
 //
-// MODE 0 (Lloyd iteration, gated) streams ONLY the points: no label array is
-// read or written.  The previous iteration's label of a point is recomputed
-// from the previous iteration's candidate list of its cell (double-buffered
-// by iteration parity, exact: the same deterministic scan that produced it),
-// so the change count -- sklearn's strict-convergence test,
-// _kmeans.py:717-723 -- costs compute instead of 4 B/point of HBM traffic.
-// Per tile: both lists in LDS (scan order = ascending centroid index, so the
-// lowest index wins ties), per-lane LDS sums for the MSLOT candidate slots
-// ranked nearest to the cell centre (k_fine), rare other winners via global
-// int64 atomics; at the tile end the slot sums are folded into the global
-// partials while the next tile's candidates are installed (2 barriers/tile).
-// MODE 1: E-step with the current centres writing labels (sorted order) and
-// the inertia into *inert_out; not gated (final E-step, relocation keys).
-template <typename T, int D, typename LT, int MODE>
-__global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__restrict__ tiles,
-                                                const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
-                                                const uint8_t *__restrict__ fc_slot) {
-    if (MODE == 0 && gated(A.ctrl)) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [TPB][AccW<D>::w]
-    __shared__ float4 nrec[CAPF], orec[CAPF];
-    __shared__ int32_t nlab[CAPF], olab[CAPF];
-    __shared__ uint8_t smap[CAPF];
-    __shared__ int32_t sinv[2][CAPF];
+// Per tile (cell): the candidate list (ascending centroid index, so the
+// strict-'<' scan keeps the lowest index on ties, _k_means_lloyd.pyx:205-213)
+// in LDS; a winner at list position j < LSLOT is summed into the lane's private
+// LDS row at slot j (ds_add_u32, no conflicts between lanes: odd row stride);
+// positions >= LSLOT (lists longer than LSLOT) use global int64 atomics.
+// Out-of-tile lanes of a partial round add into a junk slot (never read).
+// Persistent blocks walk tiles blockIdx.x, +gridDim.x, ...; the loads of the
+// next two work items (1024 points each) are in flight while one is computed.
+template <typename T, int D>
+__global__ __launch_bounds__(TPB) void k_lloyd(LloydArgs A) {
+    if (gated(A.ctrl)) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [TPB][AccL<D>::w]
+    __shared__ float4 crec[2][CAPF];
+    __shared__ int32_t cid[2][CAPF];
     const int tid = threadIdx.x;
     const unsigned G = gridDim.x;
     const unsigned nt = (unsigned)A.ntiles;
     unsigned t = blockIdx.x;
     if (t >= nt) return;
-    const unsigned iter = A.ctrl->iter;
-    const unsigned p = iter & 1u;
-    const bool first = (MODE == 0) && (iter == 0u);    // previous labels are all "-1"
-    const float4 *lrec_n = fc_rec + (size_t)p * A.lstride, *lrec_o = fc_rec + (size_t)(p ^ 1u) * A.lstride;
-    const int32_t *llab_n = fc_lab + (size_t)p * A.lstride, *llab_o = fc_lab + (size_t)(p ^ 1u) * A.lstride;
-    const uint8_t *lslot_n = fc_slot + (size_t)p * A.lstride;
-    const unsigned cl = tid < CAPF ? (unsigned)tid : (unsigned)(CAPF - 1);   // candidate lane (clamped)
-    auto tile_at = [&](unsigned i) { return tiles[i < nt ? i : nt - 1]; };
-
+    const unsigned p = A.ctrl->iter & 1u;
+    const float4 *lrec = A.fc_rec + (size_t)p * A.lstride;
+    const int32_t *llab = A.fc_lab + (size_t)p * A.lstride;
+    const unsigned cl = tid < CAPF ? (unsigned)tid : (unsigned)(CAPF - 1);
+    auto tile_at = [&](unsigned i) { return A.tiles[i < nt ? i : nt - 1]; };
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
-    const rsrc_t rl = make_rsrc(A.lab, (unsigned long long)A.npad * sizeof(LT));
+    for (int e = tid; e < AccL<D>::words; e += TPB) acc[e] = 0u;
+    uint32_t *const myacc = acc + tid * AccL<D>::w;
 
-    if (MODE == 0)
-        for (int e = tid; e < AccW<D>::words; e += TPB) acc[e] = 0u;
-
-    // Pipeline state: h = tile being computed, h1 = next tile (header known),
-    // tl2 = raw record of the tile after that; c* = h1's candidate records.
-    float4 crec, corec;
-    int clab, colab, cslot;
-    auto fetch = [&](const TileH &hh) {
+    float4 frec;
+    int flab;
+    auto fetch = [&](const TileL &hh) {
         const size_t b = (size_t)hh.cell * CAPF + cl;
-        crec = lrec_n[b];
-        clab = llab_n[b];
-        cslot = lslot_n[b];
-        if (MODE == 0) {
-            corec = lrec_o[b];
-            colab = llab_o[b];
-        }
+        frec = lrec[b];
+        flab = llab[b];
     };
-    auto install = [&](const TileH &hh, int sp) {
+    auto install = [&](const TileL &hh, int sp) {
         if (!hh.full && tid < hh.mm) {
-            nrec[tid] = crec;
-            nlab[tid] = clab;
-            smap[tid] = (uint8_t)cslot;
-            sinv[sp][cslot] = clab;
+            crec[sp][tid] = frec;
+            cid[sp][tid] = flab;
         }
-        if (hh.full && tid < MSLOT) sinv[sp][tid] = tid;
-        if (MODE == 0 && !hh.ofull && tid < hh.mo) {
-            orec[tid] = corec;
-            olab[tid] = colab;
-        }
+        if (hh.full && tid < LSLOT) cid[sp][tid] = tid;
     };
-    TileH h = make_hdr(tile_at(t), A.K, p);
+    TileL h = make_tile(tile_at(t), A.K, p);
     fetch(h);
     install(h, 0);
-    TileH h1 = make_hdr(tile_at(t + G), A.K, p);
-    TileH h2 = make_hdr(tile_at(t + 2 * G), A.K, p);
+    TileL h1 = make_tile(tile_at(t + G), A.K, p);
+    TileL h2 = make_tile(tile_at(t + 2 * G), A.K, p);
     uint4 tl3 = tile_at(t + 3 * G);
     fetch(h1);
 
     int r = 0;
-    // point offset of the work item k rounds ahead of (h, r): in h, h1 or h2
-    // (every tile has >= 1 round, k <= 2); past the last tile: out of range.
     auto item_off = [&](int k) -> unsigned {
         int rr = r + k;
         if (rr < h.nr) return h.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
         rr -= h.nr;
-        if (t + G >= nt) return 0x0ffffff0u;   // out of range (x D*sizeof(T) bytes): the buffer load returns zeros
+        if (t + G >= nt) return 0x0ffffff0u;
         if (rr < h1.nr) return h1.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
         rr -= h1.nr;
         if (t + 2 * G >= nt) return 0x0ffffff0u;
@@ -726,107 +717,67 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
     LOAD_X(xb, item_off(1));
     __syncthreads();
 
-    uint32_t nch = 0;
-    double inert = 0.0;
     unsigned long long *prep = A.partials + (size_t)(blockIdx.x % NREP) * A.K * (D + 1);
-    int par = 0;                       // sinv parity of the current tile
+    int par = 0;
 
-    // One work item (one round of h): prefetch the item two ahead into nx
-    // with unconditional loads (three register sets rotate), compute cx, and
-    // at the tile's last round fold its slot sums and install h1's candidates.
     auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx) -> bool {
         const bool last_round = (r + 1 == h.nr);
-        const bool has_next = (t + G) < nt;
         LOAD_X(nx, item_off(2));
-
-        const unsigned i0 = h.base0 + (unsigned)r * 4u * TPB + 4u * tid;
-        if (i0 < h.end) {
-            float x[4][D];
-            unpack_x<D>(cx, x);
-            bool v[4];
-            for (int e = 0; e < 4; ++e) v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
+        const unsigned rbase = h.base0 + (unsigned)r * 4u * TPB;
+        const unsigned i0 = rbase + 4u * tid;
+        float x[4][D];
+        unpack_x<D>(cx, x);
+        int bj[4];
+        if (!h.full && h.mm == 1) {
+            for (int e = 0; e < 4; ++e) bj[e] = 0;
+        } else {
             float bd[4];
-            int bj[4];
-#ifdef PCM_ABL_NOCOMPUTE
-            for (int e = 0; e < 4; ++e) { bd[e] = x[e][0]; bj[e] = 0; }
-#else
-            if (MODE == 0 && h.mm == 1) {
-                for (int e = 0; e < 4; ++e) { bd[e] = 0.f; bj[e] = 0; }
-            } else if (h.full) {
-                scan4<D>(A.C, h.mm, x, bd, bj);
-            } else {
-                scan4<D>(nrec, h.mm, x, bd, bj);
-            }
-#endif
-            int lbl[4];
-            for (int e = 0; e < 4; ++e) lbl[e] = h.full ? bj[e] : nlab[bj[e]];
-            if (MODE == 0) {
-                if (first) {
-                    for (int e = 0; e < 4; ++e) nch += v[e] ? 1u : 0u;
-                } else {
-                    float od[4];
-                    int oj[4];
-#ifdef PCM_ABL_NOCOMPUTE
-                    for (int e = 0; e < 4; ++e) oj[e] = 0;
-#else
-                    if (h.mo == 1) {
-                        for (int e = 0; e < 4; ++e) oj[e] = 0;
-                    } else if (h.ofull) {
-                        scan4<D>(A.Cold, h.mo, x, od, oj);
-                    } else {
-                        scan4<D>(orec, h.mo, x, od, oj);
-                    }
-#endif
-                    for (int e = 0; e < 4; ++e) {
-                        const int ol = h.ofull ? oj[e] : olab[oj[e]];
-                        nch += (v[e] && lbl[e] != ol) ? 1u : 0u;
-                    }
-                }
-                for (int e = 0; e < 4; ++e) {
-                    if (!v[e]) continue;
-#if defined(PCM_ABL_NOACC) || defined(PCM_ABL_NOCOMPUTE)
-                    continue;
-#endif
-                    const int sl = h.full ? bj[e] : (int)smap[bj[e]];
-                    if (sl < MSLOT) {
-                        uint32_t *ap = &acc[tid * AccW<D>::w + sl * (D + 1)];
-                        for (int a = 0; a < D; ++a) atomicAdd(ap + a, (uint32_t)fixed_i(x[e][a], A.q[a]));
-                        atomicAdd(ap + D, 1u);
-                    } else {
-                        unsigned long long *pp = prep + (size_t)lbl[e] * (D + 1);
-                        for (int a = 0; a < D; ++a)
-                            atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
-                        atomicAdd(pp + D, 1ull);
-                    }
-                }
-            } else {
-                store_l4(rl, i0, lbl, v, (RawLab<LT> *)nullptr);
-                for (int e = 0; e < 4; ++e)
-                    if (v[e]) inert += (double)bd[e];
+            if (h.full) scan4<D>(A.C, h.mm, x, bd, bj);
+            else scan4<D>(crec[par], h.mm, x, bd, bj);
+        }
+        // block-uniform: every point of the round lies inside the tile
+        const bool whole = (rbase >= h.start) && (rbase + 4u * TPB <= h.end);
+        int sl[4];
+        bool over = false;
+        for (int e = 0; e < 4; ++e) {
+            const bool v = whole || ((i0 + e >= h.start) && (i0 + e < h.end));
+            const bool hi = bj[e] >= LSLOT;
+            over |= v && hi;
+            sl[e] = (v && !hi) ? bj[e] : LSLOT;
+        }
+        for (int e = 0; e < 4; ++e) {
+            uint32_t *ap = myacc + sl[e] * (D + 1);
+            for (int a = 0; a < D; ++a) atomicAdd(ap + a, (uint32_t)fixed_i(x[e][a], A.q[a]));
+            atomicAdd(ap + D, 1u);
+        }
+        if (over) {   // list positions >= LSLOT (long lists only)
+            for (int e = 0; e < 4; ++e) {
+                const bool v = whole || ((i0 + e >= h.start) && (i0 + e < h.end));
+                if (!(v && bj[e] >= LSLOT)) continue;
+                const int lbl = h.full ? bj[e] : cid[par][bj[e]];
+                unsigned long long *pp = prep + (size_t)lbl * (D + 1);
+                for (int a = 0; a < D; ++a)
+                    atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                atomicAdd(pp + D, 1ull);
             }
         }
         if (!last_round) {
             ++r;
             return true;
         }
-        // ---- tile boundary: fold slot sums of h, install candidates of h1
+        // ---- tile boundary: fold the slot sums of h, install h1's candidates
         __syncthreads();
-        if (MODE == 0) {
-#ifdef PCM_ABL_NOFLUSH
-            const int nslots = 0;
-#else
-            const int nslots = h.mm < MSLOT ? h.mm : MSLOT;
-#endif
+        {
+            const int nslots = h.mm < LSLOT ? h.mm : LSLOT;
             const int npairs = nslots * (D + 1);
-            // 16 threads per row, each summing 16 lanes' words (stride AccW::w: conflict-free)
             for (int p0 = 0; p0 < npairs; p0 += TPB / 16) {
                 const int pi = p0 + tid / 16, sub = tid & 15;
                 long long sacc = 0;
                 if (pi < npairs) {
                     const bool cnt = (pi % (D + 1) == D);
                     for (int k = 0; k < TPB / 16; ++k) {
-                        uint32_t *ap = &acc[(sub + 16 * k) * AccW<D>::w + pi];
-                        // per-lane sums are exact int32 (<= 63 points of |xq| < 2^25)
+                        uint32_t *ap = &acc[(sub + 16 * k) * AccL<D>::w + pi];
+                        // per-lane sums are exact int32 (<= 32 points of |xq| < 2^25 per tile)
                         sacc += cnt ? (long long)*ap : (long long)(int32_t)*ap;
                         *ap = 0u;
                     }
@@ -837,18 +788,18 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
                 sacc += __shfl_down(sacc, 1, 16);
                 if (pi < npairs && sub == 0 && sacc) {
                     const int slot = pi / (D + 1), qq = pi % (D + 1);
-                    atomicAdd(prep + (size_t)sinv[par][slot] * (D + 1) + qq, (unsigned long long)sacc);
+                    atomicAdd(prep + (size_t)cid[par][slot] * (D + 1) + qq, (unsigned long long)sacc);
                 }
             }
         }
-        if (!has_next) return false;
+        if (t + G >= nt) return false;
         install(h1, par ^ 1);
         par ^= 1;
         h = h1;
         h1 = h2;
         t += G;
         r = 0;
-        h2 = make_hdr(tl3, A.K, p);
+        h2 = make_tile(tl3, A.K, p);
         tl3 = tile_at(t + 3 * G);
         fetch(h1);
         __syncthreads();
@@ -859,17 +810,9 @@ __global__ __launch_bounds__(TPB) void k_assign(AssignArgs A, const uint4 *__res
         if (!step(xb, xa)) break;
         if (!step(xc, xb)) break;
     }
-
-    if (MODE == 0) {
-        for (int o = 32; o > 0; o >>= 1) nch += __shfl_xor(nch, o);
-        if ((tid & 63) == 0 && nch) atomicAdd(&A.ctrl->changed_local, (unsigned long long)nch);
-    } else {
-        for (int o = 32; o > 0; o >>= 1) inert += __shfl_xor(inert, o);
-        if ((tid & 63) == 0) atomicAdd(A.inert_out, inert);
-    }
 }
 
-// stats[j*(D+1)+q] = sum over replicas; partials := 0; stats[K*(D+1)] = changes
+// stats[j*(D+1)+q] = sum over replicas; partials := 0; stats[K*(D+1)] = 0
 template <int D>
 __global__ __launch_bounds__(256) void k_fold(unsigned long long *__restrict__ partials, int K,
                                               unsigned long long *__restrict__ stats, Ctrl *__restrict__ ctrl) {
@@ -884,10 +827,7 @@ __global__ __launch_bounds__(256) void k_fold(unsigned long long *__restrict__ p
         }
         stats[i] = s;
     }
-    if (i == n) {
-        stats[n] = ctrl->changed_local;
-        ctrl->changed_local = 0ull;
-    }
+    if (i == n) stats[n] = 0ull;
 }
 
 // Single block of 1024 threads.  Reads the (all-reduced) statistics, halts for
@@ -896,19 +836,32 @@ __global__ __launch_bounds__(256) void k_fold(unsigned long long *__restrict__ p
 template <int D>
 __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__restrict__ stats, int K, QExp qe,
                                                  unsigned long long *__restrict__ held,
+                                                 unsigned long long *__restrict__ prev,
                                                  float4 *__restrict__ C, float4 *__restrict__ Cn,
-                                                 float4 *__restrict__ Cold,
                                                  unsigned long long *__restrict__ hist_changed,
                                                  double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl) {
     if (gated(ctrl)) return;
     const int tid = threadIdx.x;
     const int *q = qe.q;
     __shared__ unsigned cnt_empty;
+    __shared__ unsigned long long neq_s;
     __shared__ unsigned long long smax[1024];
     __shared__ int sarg[1024];
     __shared__ double ssum[1024];
-    if (tid == 0) cnt_empty = 0;
+    if (tid == 0) { cnt_empty = 0; neq_s = 0ull; }
     __syncthreads();
+    const uint32_t resume = ctrl->resume;
+    // Convergence (sklearn: labels equal, _kmeans.py:717-723): the raw statistics
+    // of this iteration (before any relocation move) equal the previous ones.
+    if (!resume) {
+        unsigned long long neq = 0;
+        for (int i = tid; i < K * (D + 1); i += 1024) {
+            const unsigned long long v = stats[i];
+            neq += (v != prev[i]) ? 1ull : 0ull;
+            prev[i] = v;
+        }
+        if (neq) atomicAdd(&neq_s, neq);
+    }
     unsigned long long bmax = 0;
     int barg = 0x7fffffff;
     unsigned ne = 0;
@@ -921,7 +874,6 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
     smax[tid] = bmax;
     sarg[tid] = barg;
     __syncthreads();
-    const uint32_t resume = ctrl->resume;
 #ifdef PCM_ABL_NOCOMPUTE
     if (false) {   // ablation build: never halt (statistics are meaningless)
 #else
@@ -933,6 +885,7 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
         if (tid == 0) {
             ctrl->halt = 1u;
             ctrl->n_empty = cnt_empty;
+            ctrl->neq_saved = neq_s;
         }
         return;
     }
@@ -982,12 +935,9 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
         if (tid < s) ssum[tid] = ssum[tid] + ssum[tid + s];
         __syncthreads();
     }
-    for (int j = tid; j < K; j += 1024) {
-        Cold[j] = C[j];
-        C[j] = Cn[j];
-    }
+    for (int j = tid; j < K; j += 1024) C[j] = Cn[j];
     if (tid == 0) {
-        const unsigned long long changed = stats[(size_t)K * (D + 1)];
+        const unsigned long long changed = resume ? ctrl->neq_saved : neq_s;
         const double shift = ssum[0];
         const uint32_t it = ctrl->iter;
         if (it < ctrl->max_iter) {

