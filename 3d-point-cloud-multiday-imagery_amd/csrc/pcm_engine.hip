@@ -597,7 +597,8 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
         constexpr int D = decltype(DD)::value;
         if (e->ntiles > 0) {
             const size_t lds = (size_t)AccL<D>::words * sizeof(uint32_t);
-            k_lloyd<TT, D><<<assign_grid(e, (const void *)k_lloyd<TT, D>, lds), TPB, lds, s>>>(A);
+            k_lloyd<TT, D><<<assign_grid(e, (const void *)k_lloyd<TT, D>, lds), TPB, lds, s>>>(A, e->tiles, e->fc_rec,
+                                                                                              e->fc_lab, e->C);
             LAUNCHCHK();
         }
         if (int rc = timing_mark(e, 2, s)) return rc;

@@ -547,12 +547,16 @@ __device__ __forceinline__ void store_l4(rsrc_t rs, unsigned off, const int (&l)
     }
 }
 
-constexpr int LSLOT = 8;
+#ifndef PCM_LSLOT
+#define PCM_LSLOT 8
+#endif
+constexpr int LSLOT = PCM_LSLOT;
 
+// Lane-minor accumulator words: word (slot, a) of thread tid at (slot*(D+1)+a)*TPB + tid,
+// so a wave's ds_add_u32 hits 32 distinct banks per half-wave whatever the slots.
 template <int D> struct AccL {
     static constexpr int rows = (LSLOT + 1) * (D + 1);   // + junk slot
-    static constexpr int w = rows | 1;
-    static constexpr int words = TPB * w;
+    static constexpr int words = TPB * rows;
 };
 
 struct LloydArgs {
@@ -652,16 +656,48 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, double *i
 //
 // Per tile (cell): the candidate list (ascending centroid index, so the
 // strict-'<' scan keeps the lowest index on ties, _k_means_lloyd.pyx:205-213)
-// in LDS; a winner at list position j < LSLOT is summed into the lane's private
-// LDS row at slot j (ds_add_u32, no conflicts between lanes: odd row stride);
+// in LDS; a winner at list position j < LSLOT is summed into the thread's
+// private LDS words of slot j (ds_add_u32, lane-minor: conflict-free);
 // positions >= LSLOT (lists longer than LSLOT) use global int64 atomics.
 // Out-of-tile lanes of a partial round add into a junk slot (never read).
 // Persistent blocks walk tiles blockIdx.x, +gridDim.x, ...; the loads of the
 // next two work items (1024 points each) are in flight while one is computed.
+//
+// The point loads are the ONLY vector-memory loads of the loop: tile headers,
+// candidate lists and the all-centre scan of FULL tiles use scalar (SMEM)
+// loads.  A vector load whose result is consumed a tile later makes the
+// compiler's waitcnt analysis fall back to vmcnt(0) at every work item, which
+// collapses the two-item prefetch (measured: 2x the kernel time).
+// Nearest of mm centres read through scalar loads (FULL tiles: the whole
+// uniform centre array); same scan order and tie rule as scan4.
+template <int D>
+__device__ __forceinline__ void scan4_s(const float4 *__restrict__ C, int mm, const float (&x)[4][D], float (&bd)[4],
+                                        int (&bj)[4]) {
+    {
+        const float4 c = C[0];
+        for (int e = 0; e < 4; ++e) { bd[e] = dist_canon<D>(x[e], c); bj[e] = 0; }
+    }
+    for (int j = 1; j < mm; ++j) {
+        const float4 c = C[j];
+        for (int e = 0; e < 4; ++e) {
+            float dd = dist_canon<D>(x[e], c);
+            bool lt = dd < bd[e];
+            bd[e] = lt ? dd : bd[e];
+            bj[e] = lt ? j : bj[e];
+        }
+    }
+}
+
+#ifndef PCM_WPE
+#define PCM_WPE 4
+#endif
 template <typename T, int D>
-__global__ __launch_bounds__(TPB) void k_lloyd(LloydArgs A) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8))) void k_lloyd(LloydArgs A, const uint4 *__restrict__ tiles,
+                                               const float4 *__restrict__ fc_rec,
+                                               const int32_t *__restrict__ fc_lab,
+                                               const float4 *__restrict__ Call) {
     if (gated(A.ctrl)) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [TPB][AccL<D>::w]
+    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LSLOT+1)*(D+1)][TPB]
     __shared__ float4 crec[2][CAPF];
     __shared__ int32_t cid[2][CAPF];
     const int tid = threadIdx.x;
@@ -670,35 +706,38 @@ __global__ __launch_bounds__(TPB) void k_lloyd(LloydArgs A) {
     unsigned t = blockIdx.x;
     if (t >= nt) return;
     const unsigned p = A.ctrl->iter & 1u;
-    const float4 *lrec = A.fc_rec + (size_t)p * A.lstride;
-    const int32_t *llab = A.fc_lab + (size_t)p * A.lstride;
-    const unsigned cl = tid < CAPF ? (unsigned)tid : (unsigned)(CAPF - 1);
-    auto tile_at = [&](unsigned i) { return A.tiles[i < nt ? i : nt - 1]; };
+    const float4 *lrec = fc_rec + (size_t)p * A.lstride;
+    const int32_t *llab = fc_lab + (size_t)p * A.lstride;
+    auto tile_at = [&](unsigned i) { return tiles[i < nt ? i : nt - 1]; };
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     for (int e = tid; e < AccL<D>::words; e += TPB) acc[e] = 0u;
-    uint32_t *const myacc = acc + tid * AccL<D>::w;
+    uint32_t *const myacc = acc + tid;
 
-    float4 frec;
-    int flab;
-    auto fetch = [&](const TileL &hh) {
-        const size_t b = (size_t)hh.cell * CAPF + cl;
-        frec = lrec[b];
-        flab = llab[b];
-    };
+    // Candidate list of tile hh into LDS half sp: scalar loads, 4 records per
+    // chunk, written by lanes 0-3 (uniform cell -> SMEM, no vector loads).
     auto install = [&](const TileL &hh, int sp) {
-        if (!hh.full && tid < hh.mm) {
-            crec[sp][tid] = frec;
-            cid[sp][tid] = flab;
+        if (hh.full) {
+            if (tid < LSLOT) cid[sp][tid] = tid;
+            return;
         }
-        if (hh.full && tid < LSLOT) cid[sp][tid] = tid;
+        const float4 *pr = lrec + (size_t)hh.cell * CAPF;
+        const int4 *pl = reinterpret_cast<const int4 *>(llab + (size_t)hh.cell * CAPF);
+        for (int j0 = 0; j0 < hh.mm; j0 += 4) {
+            const float4 v0 = pr[j0], v1 = pr[j0 + 1], v2 = pr[j0 + 2], v3 = pr[j0 + 3];
+            const int4 ids = pl[j0 >> 2];
+            if (tid < 4) {
+                const float4 v = tid == 0 ? v0 : tid == 1 ? v1 : tid == 2 ? v2 : v3;
+                const int id = tid == 0 ? ids.x : tid == 1 ? ids.y : tid == 2 ? ids.z : ids.w;
+                crec[sp][j0 + tid] = v;
+                cid[sp][j0 + tid] = id;
+            }
+        }
     };
     TileL h = make_tile(tile_at(t), A.K, p);
-    fetch(h);
     install(h, 0);
     TileL h1 = make_tile(tile_at(t + G), A.K, p);
     TileL h2 = make_tile(tile_at(t + 2 * G), A.K, p);
     uint4 tl3 = tile_at(t + 3 * G);
-    fetch(h1);
 
     int r = 0;
     auto item_off = [&](int k) -> unsigned {
@@ -728,11 +767,15 @@ __global__ __launch_bounds__(TPB) void k_lloyd(LloydArgs A) {
         float x[4][D];
         unpack_x<D>(cx, x);
         int bj[4];
-        if (!h.full && h.mm == 1) {
+#ifdef PCM_ABL_NOSCAN
+        if (true) {
+#else
+        if (h.mm == 1) {
+#endif
             for (int e = 0; e < 4; ++e) bj[e] = 0;
         } else {
             float bd[4];
-            if (h.full) scan4<D>(A.C, h.mm, x, bd, bj);
+            if (h.full) scan4_s<D>(Call, h.mm, x, bd, bj);
             else scan4<D>(crec[par], h.mm, x, bd, bj);
         }
         // block-uniform: every point of the round lies inside the tile
@@ -745,10 +788,15 @@ __global__ __launch_bounds__(TPB) void k_lloyd(LloydArgs A) {
             over |= v && hi;
             sl[e] = (v && !hi) ? bj[e] : LSLOT;
         }
+#ifdef PCM_ABL_NOACC
+        for (int e = 0; e < 4; ++e) sl[e] = (int)(x[e][0] * x[e][1] * x[e][2]) & 1;
+        for (int e = 0; e < 1; ++e) {
+#else
         for (int e = 0; e < 4; ++e) {
-            uint32_t *ap = myacc + sl[e] * (D + 1);
-            for (int a = 0; a < D; ++a) atomicAdd(ap + a, (uint32_t)fixed_i(x[e][a], A.q[a]));
-            atomicAdd(ap + D, 1u);
+#endif
+            uint32_t *ap = myacc + sl[e] * ((D + 1) * TPB);
+            for (int a = 0; a < D; ++a) atomicAdd(ap + a * TPB, (uint32_t)fixed_i(x[e][a], A.q[a]));
+            atomicAdd(ap + D * TPB, 1u);
         }
         if (over) {   // list positions >= LSLOT (long lists only)
             for (int e = 0; e < 4; ++e) {
@@ -768,16 +816,22 @@ __global__ __launch_bounds__(TPB) void k_lloyd(LloydArgs A) {
         // ---- tile boundary: fold the slot sums of h, install h1's candidates
         __syncthreads();
         {
+#ifdef PCM_ABL_NOFLUSH
+            const int nslots = 0;
+#else
             const int nslots = h.mm < LSLOT ? h.mm : LSLOT;
+#endif
             const int npairs = nslots * (D + 1);
+            // 16 threads per (slot, a) word, each summing 16 threads' words
             for (int p0 = 0; p0 < npairs; p0 += TPB / 16) {
                 const int pi = p0 + tid / 16, sub = tid & 15;
                 long long sacc = 0;
                 if (pi < npairs) {
                     const bool cnt = (pi % (D + 1) == D);
+                    uint32_t *row = acc + pi * TPB;
                     for (int k = 0; k < TPB / 16; ++k) {
-                        uint32_t *ap = &acc[(sub + 16 * k) * AccL<D>::w + pi];
-                        // per-lane sums are exact int32 (<= 32 points of |xq| < 2^25 per tile)
+                        uint32_t *ap = row + sub + 16 * k;
+                        // per-thread sums are exact int32 (<= 32 points of |xq| < 2^25 per tile)
                         sacc += cnt ? (long long)*ap : (long long)(int32_t)*ap;
                         *ap = 0u;
                     }
@@ -801,7 +855,6 @@ __global__ __launch_bounds__(TPB) void k_lloyd(LloydArgs A) {
         r = 0;
         h2 = make_tile(tl3, A.K, p);
         tl3 = tile_at(t + 3 * G);
-        fetch(h1);
         __syncthreads();
         return true;
     };
@@ -874,7 +927,7 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
     smax[tid] = bmax;
     sarg[tid] = barg;
     __syncthreads();
-#ifdef PCM_ABL_NOCOMPUTE
+#if defined(PCM_ABL_NOHALT)
     if (false) {   // ablation build: never halt (statistics are meaningless)
 #else
     if (cnt_empty > 0 && !resume) {
@@ -951,7 +1004,7 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
         if (changed == 0ull) done = 1u;
         else if (shift <= ctrl->tol) done = 2u;
         ctrl->iter = it + 1;
-#ifdef PCM_ABL_NOCOMPUTE
+#if defined(PCM_ABL_NOHALT)
         done = 0u;
 #endif
         if (!done && it + 1 >= ctrl->max_iter) done = 3u;
