@@ -54,8 +54,7 @@ struct pcm_engine {
     uint32_t *tile_off = nullptr;    // [ncells+1] first tile of each cell
     uint4 *tiles = nullptr;
     int num_cu = 256;
-    uint32_t *cc_cnt = nullptr, *cc_idx = nullptr, *fc_cnt = nullptr;
-    float4 *cc_rec = nullptr;
+    uint32_t *fc_cnt = nullptr;
     float4 *fc_rec = nullptr;
     int32_t *fc_lab = nullptr;
     float4 *C = nullptr, *Cn = nullptr;
@@ -131,14 +130,12 @@ int dispatch_l(const pcm_engine *e, F &&f) {
 }
 
 void free_layout(pcm_engine *e) {
-    void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->cc_cnt, e->cc_idx,
-                  e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->cc_rec};
+    void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
     e->tile_off = nullptr;
-    e->cc_rec = nullptr;
-    e->cc_cnt = nullptr; e->cc_idx = nullptr; e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
+    e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
     e->layout_ready = false;
     e->fit_ready = false;
 }
@@ -149,7 +146,7 @@ void choose_grid(pcm_engine *e) {
     Grid &g = e->g;
     g = Grid{};
     g.d = e->d;
-    g.F = 4;
+    g.F = 4;   // fixed: k_cand assumes 4 fine cells per coarse cell per axis
     double target = std::min(32.0 * e->k, (double)e->n / 1024.0);
     if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     target = std::max(1.0, std::min(target, (double)(1 << 18)));
@@ -331,24 +328,19 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     // 0x0ffffff0 (points) as its always-out-of-range prefetch
     if (e->npad >= 0x0ffffff0LL) return fail(PCM_E_ARG, "at most 2^28 - 32 points per engine (shard larger clouds)");
     choose_grid(e);
-    const long long nc = e->g.ncells, ncc = e->g.ncoarse;
+    const long long nc = e->g.ncells;
     const size_t ts = tsize(e->dtype);
 
     HIPCHK(hipMalloc(&e->xs, (size_t)e->d * e->npad * ts));
     HIPCHK(hipMalloc(&e->lab, (size_t)e->npad * lsize(e)));
     HIPCHK(hipMalloc(&e->perm, (size_t)std::max(1LL, n) * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->cell_start, (size_t)(nc + 1) * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->cc_cnt, (size_t)ncc * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->cc_idx, (size_t)ncc * CAPC * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->cc_rec, (size_t)ncc * CAPC * sizeof(float4)));
-    HIPCHK(hipMemsetAsync(e->cc_idx, 0, (size_t)ncc * CAPC * sizeof(uint32_t), s));
-    HIPCHK(hipMemsetAsync(e->cc_rec, 0, (size_t)ncc * CAPC * sizeof(float4), s));
     HIPCHK(hipMalloc(&e->fc_cnt, (size_t)nc * sizeof(uint32_t)));
-    // candidate lists: two parity halves (current / previous iteration)
-    HIPCHK(hipMalloc(&e->fc_rec, (size_t)2 * nc * CAPF * sizeof(float4)));
-    HIPCHK(hipMalloc(&e->fc_lab, (size_t)2 * nc * CAPF * sizeof(int32_t)));
-    HIPCHK(hipMemsetAsync(e->fc_rec, 0, (size_t)2 * nc * CAPF * sizeof(float4), s));
-    HIPCHK(hipMemsetAsync(e->fc_lab, 0, (size_t)2 * nc * CAPF * sizeof(int32_t), s));
+    // candidate lists [ncells][CAPF]
+    HIPCHK(hipMalloc(&e->fc_rec, (size_t)nc * CAPF * sizeof(float4)));
+    HIPCHK(hipMalloc(&e->fc_lab, (size_t)nc * CAPF * sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(e->fc_rec, 0, (size_t)nc * CAPF * sizeof(float4), s));
+    HIPCHK(hipMemsetAsync(e->fc_lab, 0, (size_t)nc * CAPF * sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(e->fc_cnt, 0, (size_t)nc * sizeof(uint32_t), s));
 
     if (n == 0) {
@@ -489,16 +481,8 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
 static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_coarse<D><<<(int)e->g.ncoarse, 256, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->cc_rec, e->ctrl,
-                                                      gate);
-        LAUNCHCHK();
-        int nchild = 1;
-        for (int a = 0; a < D; ++a) nchild *= e->g.F;
-        const long long fblocks = e->g.ncoarse * ((nchild + FINE_WAVES - 1) / FINE_WAVES);
-        k_fine<D><<<(int)fblocks, 64 * FINE_WAVES, 0, s>>>(e->g, e->C, e->k, e->cc_cnt, e->cc_idx, e->cc_rec,
-                                                           e->fc_cnt, e->fc_rec,
-                                                    e->fc_lab, e->tile_off, e->tiles,
-                                                    (long long)e->g.ncells * CAPF, e->ctrl, gate);
+        k_cand<D><<<(int)(e->g.ncoarse * CAND_BPC), 256, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
+                                                                 e->ctrl, gate);
         LAUNCHCHK();
         return 0;
     });
@@ -523,7 +507,7 @@ static LloydArgs lloyd_args(pcm_engine *e) {
     A.fc_rec = e->fc_rec;
     A.fc_lab = e->fc_lab;
     A.C = e->C;
-    A.lstride = (long long)e->g.ncells * CAPF;
+    A.fc_cnt = e->fc_cnt;
     A.K = e->k;
     for (int a = 0; a < MAXD; ++a) A.q[a] = e->qe.q[a];
     A.partials = e->partials;
@@ -584,10 +568,9 @@ static int timing_mark(pcm_engine *e, int which, hipStream_t s) {
     return 0;
 }
 
-int pcm_iter_local(pcm_engine *e, void *stream) {
-    if (!e) return fail(PCM_E_ARG, "null engine");
-    if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
-    hipStream_t s = (hipStream_t)stream;
+// Candidates + k_lloyd; with fold, k_fold folds the replicas into `stats`
+// (multi-GPU: the all-reduce input); without, k_global folds them itself.
+static int iter_local_impl(pcm_engine *e, hipStream_t s, bool fold) {
     if (int rc = timing_mark(e, 0, s)) return rc;
     if (int rc = launch_candidates(e, s, 1)) return rc;
     if (int rc = timing_mark(e, 1, s)) return rc;
@@ -598,29 +581,41 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
         if (e->ntiles > 0) {
             const size_t lds = (size_t)AccL<D>::words * sizeof(uint32_t);
             k_lloyd<TT, D><<<assign_grid(e, (const void *)k_lloyd<TT, D>, lds), TPB, lds, s>>>(A, e->tiles, e->fc_rec,
-                                                                                              e->fc_lab, e->C);
+                                                                                              e->fc_lab, e->C, e->fc_cnt);
             LAUNCHCHK();
         }
         if (int rc = timing_mark(e, 2, s)) return rc;
-        const int nf = e->k * (D + 1) + 1;
-        k_fold<D><<<blocks_for(nf), 256, 0, s>>>(e->partials, e->k, e->stats, e->ctrl);
-        LAUNCHCHK();
+        if (fold) {
+            const int nf = e->k * (D + 1) + 1;
+            k_fold<D><<<blocks_for(nf), 256, 0, s>>>(e->partials, e->k, e->stats, e->ctrl);
+            LAUNCHCHK();
+        }
         return 0;
+    });
+}
+
+int pcm_iter_local(pcm_engine *e, void *stream) {
+    if (!e) return fail(PCM_E_ARG, "null engine");
+    if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
+    return iter_local_impl(e, (hipStream_t)stream, true);
+}
+
+static int iter_global_impl(pcm_engine *e, hipStream_t s, bool fold) {
+    return dispatch_d(e->d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_global<D><<<1, 1024, 0, s>>>(fold ? e->partials : nullptr, e->stats, e->k, e->qe, e->held, e->prev, e->C,
+                                       e->Cn, e->hist_changed,
+                                       e->hist_shift,
+                                       e->ctrl);
+        LAUNCHCHK();
+        return timing_mark(e, 3, s);
     });
 }
 
 int pcm_iter_global(pcm_engine *e, void *stream) {
     if (!e) return fail(PCM_E_ARG, "null engine");
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
-    hipStream_t s = (hipStream_t)stream;
-    return dispatch_d(e->d, [&](auto DD) -> int {
-        constexpr int D = decltype(DD)::value;
-        k_global<D><<<1, 1024, 0, s>>>(e->stats, e->k, e->qe, e->held, e->prev, e->C, e->Cn, e->hist_changed,
-                                       e->hist_shift,
-                                       e->ctrl);
-        LAUNCHCHK();
-        return timing_mark(e, 3, s);
-    });
+    return iter_global_impl(e, (hipStream_t)stream, false);
 }
 
 int pcm_timing(pcm_engine *e, int enable) {
@@ -640,11 +635,14 @@ int pcm_timing_read(pcm_engine *e, double *ms, int *count) {
     return 0;
 }
 
+// Single-process iterations: the fold is fused into k_global (3 launches per iteration).
 int pcm_iterate(pcm_engine *e, int n, void *stream) {
     if (!e || n < 0) return fail(PCM_E_ARG, "bad argument");
+    if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
+    hipStream_t s = (hipStream_t)stream;
     for (int i = 0; i < n; ++i) {
-        if (int rc = pcm_iter_local(e, stream)) return rc;
-        if (int rc = pcm_iter_global(e, stream)) return rc;
+        if (int rc = iter_local_impl(e, s, false)) return rc;
+        if (int rc = iter_global_impl(e, s, true)) return rc;
     }
     return 0;
 }

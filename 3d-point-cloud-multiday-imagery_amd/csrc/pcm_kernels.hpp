@@ -1,7 +1,7 @@
 // pcm_kernels.hpp — gfx950 kernels of the multi-day point-cloud Lloyd engine.
 //
 // Hot path: per iteration
-//   k_coarse / k_fine  exact candidate lists per grid cell (fp64 bisector bound)
+//   k_cand             exact candidate lists per grid cell (fp64 bisector bound)
 //   k_lloyd            nearest centroid over the cell's candidates + LDS-privatised
 //                      fixed-point accumulation (replaces _k_means_lloyd.pyx:168-218)
 //   k_label            final E-step: labels + inertia (_kmeans.py:736-750)
@@ -98,8 +98,10 @@ __device__ __forceinline__ long long encode(const int *idx, const int *G, int d)
 }
 
 // fine-cell range [f0, f1] on every axis -> fp64 box containing every point binned there
+template <int D>
 __device__ __forceinline__ void cell_box(const Grid &g, const int *f0, const int *f1, double *blo, double *bhi) {
-    for (int a = 0; a < g.d; ++a) {
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
         blo[a] = g.lo[a] + (double)f0[a] * g.w[a] - g.mg[a];
         bhi[a] = (f1[a] == g.G[a] - 1) ? g.lo[a] + g.ext[a] + g.mg[a]
                                        : g.lo[a] + (double)(f1[a] + 1) * g.w[a] + g.mg[a];
@@ -270,179 +272,201 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
 }
 
 // ------------------------------------------------------------------ candidates
-// One block per coarse cell: reference r = argmin_c maxdist(c, box), keep every
-// centroid not provably dominated by r.  List ascending in centroid index.
-template <int D>
-__global__ __launch_bounds__(256) void k_coarse(Grid g, const float4 *__restrict__ C, int K,
-                                                uint32_t *__restrict__ cc_cnt, uint32_t *__restrict__ cc_idx,
-                                                float4 *__restrict__ cc_rec,
-                                                const Ctrl *__restrict__ ctrl, int gate) {
-    if (gate && gated(ctrl)) return;
-    const long long I = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (!g.prune) {
-        if (tid == 0) cc_cnt[I] = FULL;
-        return;
-    }
-    int ci[MAXD], f0[MAXD], f1[MAXD];
-    decode(I, g.GC, D, ci);
-    for (int a = 0; a < D; ++a) {
-        f0[a] = ci[a] * g.F;
-        f1[a] = min(f0[a] + g.F, g.G[a]) - 1;
-    }
-    double blo[MAXD], bhi[MAXD];
-    cell_box(g, f0, f1, blo, bhi);
-
-    double best = __builtin_inf();
-    int bj = 0x7fffffff;
-    for (int j = tid; j < K; j += 256) {
-        double m = maxdist<D>(blo, bhi, C[j]);
-        if (m < best) { best = m; bj = j; }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        double ob = __shfl_xor(best, o);
-        int oj = __shfl_xor(bj, o);
-        if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
-    }
-    __shared__ double sb[4];
-    __shared__ int sj[4];
-    __shared__ uint32_t wcnt[4];
-    if (lane == 0) { sb[wv] = best; sj[wv] = bj; }
-    __syncthreads();
-    if (tid == 0) {
-        for (int w = 1; w < 4; ++w)
-            if (sb[w] < sb[0] || (sb[w] == sb[0] && sj[w] < sj[0])) { sb[0] = sb[w]; sj[0] = sj[w]; }
-    }
-    __syncthreads();
-    const float4 r = C[sj[0]];
-    uint32_t total = 0;
-    for (int base = 0; base < K; base += 256) {
-        int j = base + tid;
-        bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r);
-        unsigned long long bal = __ballot(keep);
-        uint32_t pre = __popcll(bal & ((1ull << lane) - 1ull));
-        if (lane == 0) wcnt[wv] = __popcll(bal);
-        __syncthreads();
-        uint32_t woff = 0;
-        for (int w = 0; w < wv; ++w) woff += wcnt[w];
-        uint32_t pos = total + woff + pre;
-        if (keep && pos < (uint32_t)CAPC) {
-            cc_idx[I * CAPC + pos] = (uint32_t)j;
-            cc_rec[I * CAPC + pos] = C[j];
-        }
-        total += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        __syncthreads();
-    }
-    if (tid == 0) cc_cnt[I] = total <= (uint32_t)CAPC ? total : FULL;
-}
-
-// A cell's candidate count goes to fc_cnt and into the .w of each of its tiles
-// (so the assign kernel reaches its candidates in one dependent load).
-__device__ __forceinline__ void publish_m(long long cell, uint32_t m, uint32_t *fc_cnt, uint32_t o0, uint32_t o1,
-                                          uint4 *tiles, unsigned p) {
-    fc_cnt[cell] = m;
-    const unsigned short m16 = (m == FULL) ? (unsigned short)0xffffu : (unsigned short)m;
-    for (uint32_t o = o0; o < o1; ++o) reinterpret_cast<unsigned short *>(&tiles[o].w)[p] = m16;
-}
-
-// Fine candidate lists: one wave per fine cell, FINE_WAVES cells of the same
-// coarse parent per block (the parent list is staged in LDS once per block).
-// Reference r = the parent candidate nearest the cell centre (any centroid is
-// a valid reference; only the pruning test needs the fp64 margins).  Kept
-// candidates stay in ascending centroid order (the scan's tie rule).
-constexpr int FINE_WAVES = 4;
+// Candidate lists of every fine cell, in one launch, without global-memory
+// round trips inside the per-cell work.  Block (I, b) owns coarse cell I
+// (F^D fine cells) and children [b*cpb, (b+1)*cpb):
+//  1. coarse list (block-wide, into LDS): reference r = a centre minimising the
+//     max distance to the coarse box (LDS atomic min of a packed key: any centre
+//     is a valid reference, the choice only affects pruning power); every
+//     centre not provably dominated by r is marked in an LDS bitmap, and one
+//     wave compacts the bitmap in ascending centroid index.  More than CAPC
+//     survivors -> all K (FULL parent);
+//  2. one wave per child cell: reference = a parent candidate nearest the cell
+//     centre (again an LDS atomic-min key), keep the parent candidates it does
+//     not dominate, in ascending centroid order (the scan's tie rule); the count
+//     goes to fc_cnt[cell] (FULL = more than CAPF, or pruning disabled).
+#ifndef PCM_CAND_BPC
+#define PCM_CAND_BPC 2
+#endif
+constexpr int CAND_BPC = PCM_CAND_BPC;   // blocks per coarse cell
+constexpr int CAND_KBITS = 4096;         // bitmap capacity (larger K: direct ballot compaction)
 
 template <int D>
-__global__ __launch_bounds__(64 * FINE_WAVES) void k_fine(Grid g, const float4 *__restrict__ C, int K,
-                                                          const uint32_t *__restrict__ cc_cnt,
-                                                          const uint32_t *__restrict__ cc_idx,
-                                                          const float4 *__restrict__ cc_rec,
-                                                          uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                                          int32_t *__restrict__ fc_lab,
-                                                          const uint32_t *__restrict__ toff, uint4 *__restrict__ tiles,
-                                                          long long lstride, const Ctrl *__restrict__ ctrl, int gate) {
+__global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__ C, int K,
+                                              uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
+                                              int32_t *__restrict__ fc_lab, const Ctrl *__restrict__ ctrl, int gate) {
     if (gate && gated(ctrl)) return;
-    // lists of iteration `iter` go to parity half iter & 1
-    const unsigned p = ctrl->iter & 1u;
-    fc_rec += (size_t)p * lstride;
-    fc_lab += (size_t)p * lstride;
-    int nchild = 1;
-    for (int a = 0; a < D; ++a) nchild *= g.F;
-    const int bpc = (nchild + FINE_WAVES - 1) / FINE_WAVES;      // blocks per coarse cell
-    const long long I = blockIdx.x / bpc;
-    const int ch = (blockIdx.x % bpc) * FINE_WAVES + (threadIdx.x >> 6);
+    const long long I = blockIdx.x / CAND_BPC;
+    const int bsub = blockIdx.x % CAND_BPC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     __shared__ float4 prec[CAPC];
     __shared__ int pidx[CAPC];
+    __shared__ unsigned long long kbits[CAND_KBITS / 64];
+    __shared__ unsigned long long rkey;
+    __shared__ uint32_t wkey[4];
+    __shared__ uint32_t s_mp;
     int ci[MAXD];
     decode(I, g.GC, D, ci);
-    uint32_t mp = cc_cnt[I];
-    // the parent list is loaded speculatively (all CAPC slots, one level of loads)
-    for (uint32_t l = tid; l < (uint32_t)CAPC; l += 64 * FINE_WAVES) {
-        pidx[l] = (int)cc_idx[I * CAPC + l];
-        prec[l] = cc_rec[I * CAPC + l];
+    int nchild = 1;
+    for (int a = 0; a < D; ++a) nchild *= 4;
+    const int cpb = (nchild + CAND_BPC - 1) / CAND_BPC;
+
+    // ---- 1. coarse list
+    if (g.prune) {
+        int f0[MAXD], f1[MAXD];
+        for (int a = 0; a < D; ++a) {
+            f0[a] = ci[a] * 4;
+            f1[a] = min(f0[a] + 4, g.G[a]) - 1;
+        }
+        double blo[MAXD], bhi[MAXD];
+        cell_box<D>(g, f0, f1, blo, bhi);
+        const bool bitmap = K <= CAND_KBITS;
+        if (tid == 0) rkey = ~0ull;
+        if (bitmap)
+            for (int w = tid; w < CAND_KBITS / 64; w += 256) kbits[w] = 0ull;
+        __syncthreads();
+        unsigned long long best = ~0ull;
+        for (int j = tid; j < K; j += 256) {
+            // key: fp64 bits of a non-negative distance (monotonic), low 21 bits -> index
+            const double m = maxdist<D>(blo, bhi, C[j]);
+            const unsigned long long key = (__double_as_longlong(m) & ~0x1FFFFFull) | (unsigned long long)j;
+            best = key < best ? key : best;
+        }
+        atomicMin(&rkey, best);
+        __syncthreads();
+        const float4 r = C[(int)(rkey & 0x1FFFFFull)];
+        if (bitmap) {
+            for (int j = tid; j < K; j += 256)
+                if (!prunable<D>(blo, bhi, C[j], r)) atomicOr(&kbits[j >> 6], 1ull << (j & 63));
+            __syncthreads();
+            if (wv == 0) {
+                uint32_t total = 0;
+                for (int w = 0; w < (K + 63) / 64; ++w) {
+                    const unsigned long long word = kbits[w];
+                    const uint32_t pos = total + __popcll(word & ((1ull << lane) - 1ull));
+                    const int j = w * 64 + lane;
+                    if (((word >> lane) & 1ull) && pos < (uint32_t)CAPC) {
+                        prec[pos] = C[j];
+                        pidx[pos] = j;
+                    }
+                    total += __popcll(word);
+                }
+                if (lane == 0) s_mp = total <= (uint32_t)CAPC ? total : FULL;
+            }
+        } else {
+            // large K: ordered compaction by ballots (one barrier pair per 256 centres)
+            __shared__ uint32_t wcnt[4];
+            uint32_t total = 0;
+            for (int base = 0; base < K; base += 256) {
+                const int j = base + tid;
+                const bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r);
+                const unsigned long long bal = __ballot(keep);
+                if (lane == 0) wcnt[wv] = __popcll(bal);
+                __syncthreads();
+                uint32_t woff = 0;
+                for (int w = 0; w < wv; ++w) woff += wcnt[w];
+                const uint32_t pos = total + woff + __popcll(bal & ((1ull << lane) - 1ull));
+                if (keep && pos < (uint32_t)CAPC) {
+                    prec[pos] = C[j];
+                    pidx[pos] = j;
+                }
+                total += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+                __syncthreads();
+            }
+            if (tid == 0) s_mp = total <= (uint32_t)CAPC ? total : FULL;
+        }
+    } else if (tid == 0) {
+        s_mp = FULL;
     }
+    __syncthreads();
+    uint32_t mp = s_mp;
     const bool pfull = (mp == FULL);
     if (pfull) mp = (uint32_t)K;
-    __syncthreads();
-    if (ch >= nchild) return;
-    int f[MAXD];
-    {
-        int t = ch;
-        for (int a = D - 1; a >= 0; --a) {
-            f[a] = ci[a] * g.F + t % g.F;
-            t /= g.F;
-            if (f[a] >= g.G[a]) return;   // wave-uniform
-        }
-    }
-    const long long cell = encode(f, g.G, D);
-    const uint32_t to0 = toff[cell], to1 = toff[cell + 1];   // issued early, used at the end
-    if (!g.prune) {
-        if (lane == 0) publish_m(cell, FULL, fc_cnt, to0, to1, tiles, p);
-        return;
-    }
-    double blo[MAXD], bhi[MAXD];
-    cell_box(g, f, f, blo, bhi);
-    float ctr[MAXD];
-    for (int a = 0; a < D; ++a) ctr[a] = (float)(0.5 * (blo[a] + bhi[a]));
-    // reference: nearest parent candidate to the centre (fp32, lowest index on ties)
-    float best = __builtin_inff();
-    int bj = 0x7fffffff;   // list position of the reference (positions ascend with centroid index)
-    for (uint32_t l = lane; l < mp; l += 64) {
-        const float4 c = pfull ? C[l] : prec[l];
-        float dsum = 0.f;
-        for (int a = 0; a < D; ++a) {
-            const float dd = ctr[a] - comp(c, a);
-            dsum += dd * dd;
-        }
-        if (dsum < best || (dsum == best && (int)l < bj)) { best = dsum; bj = (int)l; }
-    }
-    for (int sft = 32; sft > 0; sft >>= 1) {
-        const float ob = __shfl_xor(best, sft);
-        const int oj = __shfl_xor(bj, sft);
-        if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
-    }
-    const float4 r = pfull ? C[bj] : prec[bj];
-    uint32_t total = 0;
-    for (uint32_t base = 0; base < mp; base += 64) {
-        const uint32_t l = base + lane;
-        const bool in = l < mp;
-        const float4 c = in ? (pfull ? C[l] : prec[l]) : r;
-        const int j = in ? (pfull ? (int)l : pidx[l]) : 0;
-#ifdef PCM_DBG_NOPRUNE_FINE
-        const bool keep = in;
-#else
-        const bool keep = in && !prunable<D>(blo, bhi, c, r);
+#ifdef PCM_ABL_COARSEONLY
+    if (mp != 12345u) return;
 #endif
-        const unsigned long long bal = __ballot(keep);
-        const uint32_t pos = total + __popcll(bal & ((1ull << lane) - 1ull));
-        if (keep && pos < (uint32_t)CAPF) {
-            fc_rec[cell * CAPF + pos] = c;
-            fc_lab[cell * CAPF + pos] = j;
+
+    // ---- 2. one wave per child cell (F = 4 children per axis)
+    auto child = [&](auto PFc) {
+        constexpr bool PF = decltype(PFc)::value;
+        for (int ch = bsub * cpb + wv; ch < min(nchild, (bsub + 1) * cpb); ch += 4) {
+            int f[MAXD];
+            bool inside = true;
+#pragma unroll
+            for (int a = D - 1, t = ch; a >= 0; --a, t >>= 2) {
+                f[a] = ci[a] * 4 + (t & 3);
+                inside &= f[a] < g.G[a];
+            }
+            if (!inside) continue;   // wave-uniform
+            const long long cell = encode(f, g.G, D);
+            if (!g.prune) {
+                if (lane == 0) fc_cnt[cell] = FULL;
+                continue;
+            }
+            double blo[MAXD], bhi[MAXD];
+            cell_box<D>(g, f, f, blo, bhi);
+            float ctr[MAXD];
+#pragma unroll
+            for (int a = 0; a < D; ++a) ctr[a] = (float)(0.5 * (blo[a] + bhi[a]));
+            // reference: a parent candidate nearest the centre
+            int bl;
+            if constexpr (PF) {   // exact wave argmin (K may exceed a packed key's index field)
+                float bd = __builtin_inff();
+                bl = 0x7fffffff;
+                for (uint32_t l = lane; l < mp; l += 64) {
+                    const float4 c = C[l];
+                    float dsum = 0.f;
+#pragma unroll
+                    for (int a = 0; a < D; ++a) {
+                        const float dd = ctr[a] - comp(c, a);
+                        dsum += dd * dd;
+                    }
+                    if (dsum < bd) { bd = dsum; bl = (int)l; }
+                }
+                for (int sft = 32; sft > 0; sft >>= 1) {
+                    const float ob = __shfl_xor(bd, sft);
+                    const int ol = __shfl_xor(bl, sft);
+                    if (ob < bd || (ob == bd && ol < bl)) { bd = ob; bl = ol; }
+                }
+            } else {   // key = distance bits (low byte dropped) | list position (< CAPC)
+                if (lane == 0) wkey[wv] = ~0u;
+                uint32_t best = ~0u;
+                for (uint32_t l = lane; l < mp; l += 64) {
+                    const float4 c = prec[l];
+                    float dsum = 0.f;
+#pragma unroll
+                    for (int a = 0; a < D; ++a) {
+                        const float dd = ctr[a] - comp(c, a);
+                        dsum += dd * dd;
+                    }
+                    const uint32_t key = (__float_as_uint(dsum) & 0xFFFFFF00u) | l;
+                    best = key < best ? key : best;
+                }
+                atomicMin(&wkey[wv], best);
+                bl = (int)(wkey[wv] & 0xFFu);
+            }
+            const float4 r = PF ? C[bl] : prec[bl];
+            uint32_t total = 0;
+            for (uint32_t base = 0; base < mp; base += 64) {
+                const uint32_t l = base + lane;
+                const bool in = l < mp;
+                const uint32_t lc = in ? l : (uint32_t)bl;
+                const float4 c = PF ? C[lc] : prec[lc];
+                const int j = PF ? (int)lc : pidx[lc];
+                const bool keep = in && !prunable<D>(blo, bhi, c, r);
+                const unsigned long long bal = __ballot(keep);
+                const uint32_t pos = total + __popcll(bal & ((1ull << lane) - 1ull));
+                if (keep && pos < (uint32_t)CAPF) {
+                    fc_rec[cell * CAPF + pos] = c;
+                    fc_lab[cell * CAPF + pos] = j;
+                }
+                total += __popcll(bal);
+            }
+            if (lane == 0) fc_cnt[cell] = total <= (uint32_t)CAPF ? total : FULL;
         }
-        total += __popcll(bal);
-    }
-    if (lane == 0) publish_m(cell, total <= (uint32_t)CAPF ? total : FULL, fc_cnt, to0, to1, tiles, p);
+    };
+    if (pfull) child(std::integral_constant<bool, true>{});
+    else child(std::integral_constant<bool, false>{});
 }
 
 // ------------------------------------------------------------------ assign
@@ -562,12 +586,12 @@ template <int D> struct AccL {
 struct LloydArgs {
     const void *xs;                 // packed AoS [npad][D] of T, cell order
     long long npad;
-    const uint4 *tiles;             // {cell, start, end, m0 | m1 << 16}; m_p written by k_fine (parity p)
+    const uint4 *tiles;             // {cell, start, end, -}
+    const uint32_t *fc_cnt;         // candidate count per cell (FULL: all K)
     long long ntiles;
     const float4 *fc_rec;
     const int32_t *fc_lab;
     const float4 *C;                // all centres (FULL cells)
-    long long lstride;              // distance between the two parity halves of fc_*
     int K;
     int q[MAXD];
     unsigned long long *partials;   // [NREP][K][D+1]
@@ -579,14 +603,14 @@ struct TileL {
     int mm, full, nr, pad_;
 };
 
-__device__ __forceinline__ TileL make_tile(const uint4 &t, int K, unsigned p) {
+// t.w = the cell's candidate count (fc_cnt[t.x], or FULL)
+__device__ __forceinline__ TileL make_tile(const uint4 &t, int K) {
     TileL h;
     h.cell = t.x;
     h.start = t.y;
     h.end = t.z;
-    const unsigned mn = p ? (t.w >> 16) : (t.w & 0xffffu);
-    h.full = (mn == 0xffffu) ? 1 : 0;
-    h.mm = h.full ? K : (int)mn;
+    h.full = (t.w == FULL) ? 1 : 0;
+    h.mm = h.full ? K : (int)t.w;
     h.base0 = h.start & ~3u;
     h.nr = (int)((h.end - h.base0 + 4 * TPB - 1) / (4 * TPB));
     h.pad_ = 0;
@@ -604,14 +628,15 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, double *i
     const int tid = threadIdx.x;
     const unsigned G = gridDim.x;
     const unsigned nt = (unsigned)A.ntiles;
-    const unsigned p = A.ctrl->iter & 1u;
-    const float4 *lrec = A.fc_rec + (size_t)p * A.lstride;
-    const int32_t *llab = A.fc_lab + (size_t)p * A.lstride;
+    const float4 *lrec = A.fc_rec;
+    const int32_t *llab = A.fc_lab;
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     const rsrc_t rl = make_rsrc(lab, (unsigned long long)A.npad * sizeof(LT));
     double inert = 0.0;
     for (unsigned t = blockIdx.x; t < nt; t += G) {
-        const TileL h = make_tile(A.tiles[t], A.K, p);
+        uint4 tr = A.tiles[t];
+        tr.w = A.fc_cnt[tr.x];
+        const TileL h = make_tile(tr, A.K);
         __syncthreads();
         if (!h.full && tid < h.mm) {
             crec[tid] = lrec[(size_t)h.cell * CAPF + tid];
@@ -695,7 +720,8 @@ template <typename T, int D>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8))) void k_lloyd(LloydArgs A, const uint4 *__restrict__ tiles,
                                                const float4 *__restrict__ fc_rec,
                                                const int32_t *__restrict__ fc_lab,
-                                               const float4 *__restrict__ Call) {
+                                               const float4 *__restrict__ Call,
+                                               const uint32_t *__restrict__ fc_cnt) {
     if (gated(A.ctrl)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LSLOT+1)*(D+1)][TPB]
     __shared__ float4 crec[2][CAPF];
@@ -705,10 +731,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     const unsigned nt = (unsigned)A.ntiles;
     unsigned t = blockIdx.x;
     if (t >= nt) return;
-    const unsigned p = A.ctrl->iter & 1u;
-    const float4 *lrec = fc_rec + (size_t)p * A.lstride;
-    const int32_t *llab = fc_lab + (size_t)p * A.lstride;
-    auto tile_at = [&](unsigned i) { return tiles[i < nt ? i : nt - 1]; };
+    const float4 *lrec = fc_rec;
+    const int32_t *llab = fc_lab;
+    // tile record with .w := the cell's candidate count (dependent scalar load)
+    auto tile_at = [&](unsigned i) {
+        uint4 v = tiles[i < nt ? i : nt - 1];
+        v.w = fc_cnt[v.x];
+        return v;
+    };
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     for (int e = tid; e < AccL<D>::words; e += TPB) acc[e] = 0u;
     uint32_t *const myacc = acc + tid;
@@ -733,10 +763,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
             }
         }
     };
-    TileL h = make_tile(tile_at(t), A.K, p);
+    TileL h = make_tile(tile_at(t), A.K);
     install(h, 0);
-    TileL h1 = make_tile(tile_at(t + G), A.K, p);
-    TileL h2 = make_tile(tile_at(t + 2 * G), A.K, p);
+    TileL h1 = make_tile(tile_at(t + G), A.K);
+    TileL h2 = make_tile(tile_at(t + 2 * G), A.K);
     uint4 tl3 = tile_at(t + 3 * G);
 
     int r = 0;
@@ -853,7 +883,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         h1 = h2;
         t += G;
         r = 0;
-        h2 = make_tile(tl3, A.K, p);
+        h2 = make_tile(tl3, A.K);
         tl3 = tile_at(t + 3 * G);
         __syncthreads();
         return true;
@@ -883,49 +913,87 @@ __global__ __launch_bounds__(256) void k_fold(unsigned long long *__restrict__ p
     if (i == n) stats[n] = 0ull;
 }
 
-// Single block of 1024 threads.  Reads the (all-reduced) statistics, halts for
-// relocation when a cluster is empty (unless resuming), otherwise averages,
-// computes the shift with the fixed reduction tree and sets convergence flags.
+// Single block of 1024 threads.  Optionally first folds the NREP replicas of
+// the partials into `stats` (single-GPU path: no all-reduce in between).  Then
+// reads the (all-reduced) statistics, halts for relocation when a cluster is
+// empty (unless resuming), otherwise averages, computes the shift with the
+// fixed reduction tree (per-thread sums over j = tid + 1024 r, then the halving
+// tree 512..1, as oracle/lloyd_ref.py shift_total) and sets convergence flags.
 template <int D>
-__global__ __launch_bounds__(1024) void k_global(const unsigned long long *__restrict__ stats, int K, QExp qe,
+__global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict__ partials,
+                                                 unsigned long long *__restrict__ stats, int K, QExp qe,
                                                  unsigned long long *__restrict__ held,
                                                  unsigned long long *__restrict__ prev,
                                                  float4 *__restrict__ C, float4 *__restrict__ Cn,
                                                  unsigned long long *__restrict__ hist_changed,
                                                  double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl) {
     if (gated(ctrl)) return;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int *q = qe.q;
+    const int n = K * (D + 1);
     __shared__ unsigned cnt_empty;
     __shared__ unsigned long long neq_s;
-    __shared__ unsigned long long smax[1024];
-    __shared__ int sarg[1024];
+    __shared__ unsigned long long wmax[16];
+    __shared__ int warg[16];
     __shared__ double ssum[1024];
     if (tid == 0) { cnt_empty = 0; neq_s = 0ull; }
     __syncthreads();
     const uint32_t resume = ctrl->resume;
+    // Thread tid owns centroids j = tid + 1024 r: every load of a row (its NREP
+    // replicas, the previous statistics) is issued before any is consumed, so a
+    // pass costs one memory round trip.
     // Convergence (sklearn: labels equal, _kmeans.py:717-723): the raw statistics
     // of this iteration (before any relocation move) equal the previous ones.
-    if (!resume) {
-        unsigned long long neq = 0;
-        for (int i = tid; i < K * (D + 1); i += 1024) {
-            const unsigned long long v = stats[i];
-            neq += (v != prev[i]) ? 1ull : 0ull;
-            prev[i] = v;
-        }
-        if (neq) atomicAdd(&neq_s, neq);
-    }
-    unsigned long long bmax = 0;
+    unsigned long long neq = 0, bmax = 0;
     int barg = 0x7fffffff;
     unsigned ne = 0;
     for (int j = tid; j < K; j += 1024) {
-        unsigned long long c = stats[(size_t)j * (D + 1) + D];
+        unsigned long long row[D + 1], pv[D + 1];
+        const size_t o = (size_t)j * (D + 1);
+        if (partials) {
+            unsigned long long part[NREP][D + 1];
+#pragma unroll
+            for (int r = 0; r < NREP; ++r)
+#pragma unroll
+                for (int a = 0; a <= D; ++a) part[r][a] = partials[(size_t)r * n + o + a];
+#pragma unroll
+            for (int a = 0; a <= D; ++a) pv[a] = prev[o + a];
+#pragma unroll
+            for (int a = 0; a <= D; ++a) {
+                row[a] = 0ull;
+#pragma unroll
+                for (int r = 0; r < NREP; ++r) row[a] += part[r][a];
+            }
+#pragma unroll
+            for (int r = 0; r < NREP; ++r)
+#pragma unroll
+                for (int a = 0; a <= D; ++a) partials[(size_t)r * n + o + a] = 0ull;
+#pragma unroll
+            for (int a = 0; a <= D; ++a) stats[o + a] = row[a];
+        } else {
+#pragma unroll
+            for (int a = 0; a <= D; ++a) { row[a] = stats[o + a]; pv[a] = prev[o + a]; }
+        }
+        if (!resume) {
+#pragma unroll
+            for (int a = 0; a <= D; ++a) {
+                neq += (row[a] != pv[a]) ? 1ull : 0ull;
+                prev[o + a] = row[a];
+            }
+        }
+        const unsigned long long c = row[D];
         if (c == 0) ne++;
         if (c > bmax) { bmax = c; barg = j; }
     }
-    atomicAdd(&cnt_empty, ne);
-    smax[tid] = bmax;
-    sarg[tid] = barg;
+    if (partials && tid == 0) stats[n] = 0ull;
+    if (neq) atomicAdd(&neq_s, neq);
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long ob = __shfl_xor(bmax, o);
+        const int oa = __shfl_xor(barg, o);
+        if (ob > bmax || (ob == bmax && oa < barg)) { bmax = ob; barg = oa; }
+    }
+    if (lane == 0) { wmax[wv] = bmax; warg[wv] = barg; }
+    if (ne) atomicAdd(&cnt_empty, ne);
     __syncthreads();
 #if defined(PCM_ABL_NOHALT)
     if (false) {   // ablation build: never halt (statistics are meaningless)
@@ -934,7 +1002,7 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
 #endif
         // Snapshot the reduced statistics: the no-op iterations queued behind a
         // halt still run their all-reduce on `stats`.
-        for (int i = tid; i < K * (D + 1) + 1; i += 1024) held[i] = stats[i];
+        for (int i = tid; i < n + 1; i += 1024) held[i] = stats[i];
         if (tid == 0) {
             ctrl->halt = 1u;
             ctrl->n_empty = cnt_empty;
@@ -942,73 +1010,92 @@ __global__ __launch_bounds__(1024) void k_global(const unsigned long long *__res
         }
         return;
     }
-    for (int s = 512; s > 0; s >>= 1) {
-        if (tid < s) {
-            unsigned long long o = smax[tid + s];
-            int oa = sarg[tid + s];
-            if (o > smax[tid] || (o == smax[tid] && oa < sarg[tid])) { smax[tid] = o; sarg[tid] = oa; }
-        }
-        __syncthreads();
-    }
-    const int argmax = sarg[0];
-    // average
-    for (int j = tid; j < K; j += 1024) {
-        const unsigned long long c = stats[(size_t)j * (D + 1) + D];
+    unsigned long long gmax = wmax[0];
+    int argmax = warg[0];
+    for (int w = 1; w < 16; ++w)
+        if (wmax[w] > gmax || (wmax[w] == gmax && warg[w] < argmax)) { gmax = wmax[w]; argmax = warg[w]; }
+    // average + shift (thread tid owns j = tid + 1024 r in every loop below);
+    // shift: per-thread sequential sum over its j, then the fixed tree below
+    auto average_row = [&](int j, float4 &cn) -> bool {
+        unsigned long long row[D + 1];
+#pragma unroll
+        for (int a = 0; a <= D; ++a) row[a] = stats[(size_t)j * (D + 1) + a];
+        const unsigned long long c = row[D];
         float out[4] = {0.f, 0.f, 0.f, 0.f};
         if (c > 0) {
+#pragma unroll
             for (int a = 0; a < D; ++a) {
-                const long long sv = (long long)stats[(size_t)j * (D + 1) + a];   // exact signed sum
+                const long long sv = (long long)row[a];   // exact signed sum
                 const double m = ((double)sv * __builtin_ldexp(1.0, -q[a])) / (double)c;
                 out[a] = (float)m;
             }
-            Cn[j] = make_float4(out[0], out[1], out[2], out[3]);
         }
-    }
-    __syncthreads();
-    for (int j = tid; j < K; j += 1024) {
-        const unsigned long long c = stats[(size_t)j * (D + 1) + D];
-        if (c == 0) Cn[j] = (smax[0] > 0) ? Cn[argmax] : C[j];
-    }
-    __syncthreads();
-    // shift: per-thread sequential over j = tid + 1024 r, then halving tree
-    double acc = 0.0;
-    for (int j = tid; j < K; j += 1024) {
-        const float4 a4 = Cn[j], b4 = C[j];
-        double s = 0.0;
+        cn = make_float4(out[0], out[1], out[2], out[3]);
+        return c > 0;
+    };
+    auto shift_of = [&](const float4 &a4, const float4 &b4) -> double {
+        double sh = 0.0;
+#pragma unroll
         for (int a = 0; a < D; ++a) {
-            double dd = (double)comp(a4, a) - (double)comp(b4, a);
-            double sq = dd * dd;
-            s = (a == 0) ? sq : s + sq;
+            const double dd = (double)comp(a4, a) - (double)comp(b4, a);
+            const double sq = dd * dd;
+            sh = (a == 0) ? sq : sh + sq;
         }
-        acc = acc + s;
+        return sh;
+    };
+    double acc = 0.0;
+    if (cnt_empty == 0) {   // the common case: no empty cluster, one pass
+        for (int j = tid; j < K; j += 1024) {
+            const float4 b4 = C[j];
+            float4 cn;
+            average_row(j, cn);
+            acc = acc + shift_of(cn, b4);
+            C[j] = cn;
+        }
+    } else {   // resumed after relocation: an empty cluster copies the largest one's centre
+        for (int j = tid; j < K; j += 1024) {
+            float4 cn;
+            if (average_row(j, cn)) Cn[j] = cn;
+        }
+        __syncthreads();   // Cn[argmax] is read by other threads
+        for (int j = tid; j < K; j += 1024) {
+            const unsigned long long c = stats[(size_t)j * (D + 1) + D];
+            if (c == 0) Cn[j] = (gmax > 0) ? Cn[argmax] : C[j];
+            const float4 a4 = Cn[j], b4 = C[j];
+            acc = acc + shift_of(a4, b4);
+            C[j] = Cn[j];
+        }
     }
     ssum[tid] = acc;
     __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
-        if (tid < s) ssum[tid] = ssum[tid] + ssum[tid + s];
+    for (int st = 512; st >= 64; st >>= 1) {
+        if (tid < st) ssum[tid] = ssum[tid] + ssum[tid + st];
         __syncthreads();
     }
-    for (int j = tid; j < K; j += 1024) C[j] = Cn[j];
-    if (tid == 0) {
-        const unsigned long long changed = resume ? ctrl->neq_saved : neq_s;
-        const double shift = ssum[0];
-        const uint32_t it = ctrl->iter;
-        if (it < ctrl->max_iter) {
-            hist_changed[it] = changed;
-            hist_shift[it] = shift;
-        }
-        ctrl->last_changed = changed;
-        ctrl->last_shift = shift;
-        ctrl->resume = 0u;
-        uint32_t done = 0;
-        if (changed == 0ull) done = 1u;
-        else if (shift <= ctrl->tol) done = 2u;
-        ctrl->iter = it + 1;
+    if (wv == 0) {
+        double v = ssum[lane];
+        for (int st = 32; st > 0; st >>= 1) v = v + __shfl_down(v, st);   // lane t: v_t + v_{t+st}
+        if (lane == 0) {
+            const unsigned long long changed = resume ? ctrl->neq_saved : neq_s;
+            const double shift = v;
+            const uint32_t it = ctrl->iter;
+            if (it < ctrl->max_iter) {
+                hist_changed[it] = changed;
+                hist_shift[it] = shift;
+            }
+            ctrl->last_changed = changed;
+            ctrl->last_shift = shift;
+            ctrl->resume = 0u;
+            uint32_t done = 0;
+            if (changed == 0ull) done = 1u;
+            else if (shift <= ctrl->tol) done = 2u;
+            ctrl->iter = it + 1;
 #if defined(PCM_ABL_NOHALT)
-        done = 0u;
+            done = 0u;
 #endif
-        if (!done && it + 1 >= ctrl->max_iter) done = 3u;
-        ctrl->done = done;
+            if (!done && it + 1 >= ctrl->max_iter) done = 3u;
+            ctrl->done = done;
+        }
     }
 }
 
