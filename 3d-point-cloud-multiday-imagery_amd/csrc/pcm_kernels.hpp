@@ -770,15 +770,28 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     uint4 tl3 = tile_at(t + 3 * G);
 
     int r = 0;
+    // Lanes past their tile's end get the out-of-range offset: the buffer load
+    // returns zeros without touching memory (no re-read of the next cell's rows).
     auto item_off = [&](int k) -> unsigned {
         int rr = r + k;
-        if (rr < h.nr) return h.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
-        rr -= h.nr;
-        if (t + G >= nt) return 0x0ffffff0u;
-        if (rr < h1.nr) return h1.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
-        rr -= h1.nr;
-        if (t + 2 * G >= nt) return 0x0ffffff0u;
-        return h2.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
+        unsigned o, e;
+        if (rr < h.nr) {
+            o = h.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
+            e = h.end;
+        } else {
+            rr -= h.nr;
+            if (t + G >= nt) return 0x0ffffff0u;
+            if (rr < h1.nr) {
+                o = h1.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
+                e = h1.end;
+            } else {
+                rr -= h1.nr;
+                if (t + 2 * G >= nt) return 0x0ffffff0u;
+                o = h2.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
+                e = h2.end;
+            }
+        }
+        return o < e ? o : 0x0ffffff0u;
     };
 
     Raw<T, D> xa, xb, xc;

@@ -64,6 +64,21 @@ def cpu_baseline(k: int, d: int, budget_s: float = 12.0) -> dict:
                       f"(-O3 -ffp-contract=off, OpenMP {threads} threads, {cpu_model})"}
 
 
+def pmc_traffic(n, k, d, world):
+    """HBM bytes per k_lloyd launch from a rocprofv3 --pmc summary of this same
+    workload (tools/evidence.sh; FETCH_SIZE x2 for gfx950's halved wide-read
+    count, + WRITE_SIZE, per MI355X_MICROARCH.md), or None."""
+    path = os.environ.get("PCM_PMC_JSON") or os.path.join(ROOT, "profiles", "pmc_k_lloyd.json")
+    if world != 1 or (n, k, d) != (100_000_000, 1024, 3) or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        pm = json.load(f)
+    rd, wr = pm.get("hbm_read_bytes_corrected"), pm.get("hbm_write_bytes")
+    if rd is None or wr is None:
+        return None, None
+    return rd + wr, os.path.relpath(path, ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,6 +177,7 @@ def main():
         # the iteration kernel streams only the points (labels are recomputed, not stored)
         bytes_pt = D * 4
         achieved = bytes_pt * n_local / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(N, K, D, world)
         value = N * args.steps / dt
         out = {
             "metric": METRIC,
@@ -182,7 +198,7 @@ def main():
                        "n_points": N, "k": K, "d": D, "parallelism": f"row-shard dp{world}",
                        "cells": info["ncells"], "tiles": info["ntiles"], "grid": info["grid"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_lloyd<float,3>",
                          "algorithmic_bytes_per_point": bytes_pt,
                          "avg_launch_ms": assign_ms},
