@@ -7,6 +7,7 @@ Cloud" plugin (see DESIGN.md / INTEGRATION.md).  Import name: ``pcm_amd``
 Public API
 ----------
 lloyd_fit(X, centers_init, max_iter, tol, group=None)  -> LloydResult
+kmeans_plusplus(X, n_clusters, random_state=...)       -> (centers, indices), GPU k-means++
 kmeans_fuse(clouds, n_clusters, ...)                   -> napari layer tuples
 HeightMapExtractor                                     -> SatellitePlugin drop-in
 Engine                                                 -> the C-ABI engine wrapper
@@ -15,7 +16,7 @@ from .fixed import QBITS, fixed_q  # noqa: F401
 from .lloyd import LloydResult, lloyd_fit  # noqa: F401
 
 __all__ = ["lloyd_fit", "LloydResult", "fixed_q", "QBITS", "Engine", "kmeans_fuse", "HeightMapExtractor",
-           "build_library"]
+           "build_library", "kmeans_plusplus"]
 
 
 def __getattr__(name):
@@ -26,6 +27,9 @@ def __getattr__(name):
     if name in ("kmeans_fuse", "HeightMapExtractor", "PREFIX"):
         from . import plugin
         return getattr(plugin, name)
+    if name == "kmeans_plusplus":
+        from .kpp import kmeans_plusplus
+        return kmeans_plusplus
     if name == "build_library":
         from ._lib import build
         return build

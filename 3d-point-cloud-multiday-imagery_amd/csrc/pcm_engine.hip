@@ -15,6 +15,7 @@
 #include <string>
 
 #include "pcm_kernels.hpp"
+#include "pcm_kpp.hpp"
 #include "pcm_kmeans.h"
 
 using namespace pcm;
@@ -874,6 +875,61 @@ int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int 
         LAUNCHCHK();
         return 0;
     });
+}
+
+// k-means++ seeding (oracle/kpp_ref.py; sklearn/cluster/_kmeans.py:174-272).
+int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, int64_t first_index,
+                 const uint64_t *umant, int scale, int64_t *indices, void *stream) {
+    if (!X || !indices || n < 1 || k < 1 || k > n || d < 1 || d > MAXD) return fail(PCM_E_ARG, "bad argument");
+    if (n_local_trials < 1 || n_local_trials > KPP_LMAX) return fail(PCM_E_ARG, "n_local_trials must be 1..16");
+    if (first_index < 0 || first_index >= n) return fail(PCM_E_ARG, "first_index out of range");
+    if (k > 1 && !umant) return fail(PCM_E_ARG, "umant is null");
+    hipStream_t s = (hipStream_t)stream;
+    const long long nblk = (n + KPP_BS - 1) / KPP_BS;
+    const int L = n_local_trials;
+    float *closest = nullptr;
+    unsigned long long *bsum = nullptr, *um = nullptr;
+    KppState *st = nullptr;
+    int rc = 0;
+    do {
+        hipError_t err;
+        if ((err = hipMalloc(&closest, (size_t)n * sizeof(float))) ||
+            (err = hipMalloc(&bsum, (size_t)nblk * KPP_LMAX * sizeof(unsigned long long))) ||
+            (err = hipMalloc(&st, sizeof(KppState))) ||
+            (err = hipMalloc(&um, (size_t)std::max(1, (k - 1) * L) * sizeof(unsigned long long)))) {
+            rc = fail(PCM_E_NOMEM, std::string("kmeanspp workspace: ") + hipGetErrorString(err));
+            break;
+        }
+        if (k > 1 && (err = hipMemcpyAsync(um, umant, (size_t)(k - 1) * L * sizeof(unsigned long long),
+                                           hipMemcpyHostToDevice, s))) {
+            rc = fail(PCM_E_HIP, "kmeanspp uniforms upload");
+            break;
+        }
+        rc = dispatch_d(d, [&](auto DD) -> int {
+            constexpr int D = decltype(DD)::value;
+            k_kpp_init<D><<<1, 64, 0, s>>>(X, first_index, st);
+            LAUNCHCHK();
+            for (int c = 0; c < k; ++c) {
+                k_kpp_pass<D><<<(int)nblk, 256, 0, s>>>(X, n, closest, st, scale, bsum);
+                LAUNCHCHK();
+                const bool more = c + 1 < k;
+                k_kpp_select<<<1, 1024, 0, s>>>(bsum, nblk, st, (long long *)indices, c,
+                                                more ? um + (size_t)c * L : nullptr, L);
+                LAUNCHCHK();
+                if (more) {
+                    k_kpp_locate<D><<<L, 1024, 0, s>>>(X, n, closest, st, scale);
+                    LAUNCHCHK();
+                }
+            }
+            return 0;
+        });
+        if (rc) break;
+        if ((err = hipStreamSynchronize(s))) rc = fail(PCM_E_HIP, std::string("kmeanspp: ") + hipGetErrorString(err));
+    } while (0);
+    void *ps[] = {closest, bsum, st, um};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    return rc;
 }
 
 }  // extern "C"

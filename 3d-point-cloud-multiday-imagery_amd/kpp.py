@@ -1,0 +1,68 @@
+"""k-means++ seeding on the GPU.
+
+``kmeans_plusplus`` mirrors ``sklearn.cluster.kmeans_plusplus`` (same
+arguments, same ``(centers, indices)`` result, same random stream: a seeded
+``RandomState`` yields the indices scikit-learn yields on the same cloud, up to
+the canonical-arithmetic caveat of oracle/kpp_ref.py).  The host draws the
+random numbers exactly as ``_kmeans_plusplus`` consumes them
+(sklearn/cluster/_kmeans.py:215-248) and the HIP kernels of ``csrc/pcm_kpp.hpp``
+do every pass over the cloud; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import _ptr, _stream
+
+
+def _scale(n: int, maxd: float) -> int:
+    """Weight exponent: n * 2**s * maxd (with rounding margin) < 2**62."""
+    if maxd <= 0 or n <= 0:
+        return 0
+    _, e = math.frexp(maxd * (1.0 + 2.0 ** -20))
+    return int(62 - max(1, int(n - 1).bit_length()) - e)
+
+
+def _first_index(n: int, u0: float) -> int:
+    """numpy RandomState.choice(n, p=ones/n) for its single random_sample() draw u0."""
+    p = np.full(n, 1.0 / n)
+    cdf = p.cumsum()
+    cdf /= cdf[-1]
+    return int(cdf.searchsorted(u0, side="right"))
+
+
+def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_local_trials=None):
+    """GPU k-means++ of a (n, d) cloud on a HIP device; returns (centers (k, d) float32, indices int64)."""
+    if not (isinstance(X, torch.Tensor) and X.is_cuda):
+        raise _lib.PcmError("kmeans_plusplus expects a HIP device tensor (no CPU fallback)")
+    if X.dim() != 2 or not 1 <= X.shape[1] <= 4:
+        raise ValueError("X must be (n, d) with 1 <= d <= 4")
+    Xf = X.to(torch.float32).contiguous()
+    n, d = Xf.shape
+    k = int(n_clusters)
+    if not 1 <= k <= n:
+        raise ValueError(f"n_samples={n} should be >= n_clusters={k}")
+    if not torch.isfinite(Xf).all():
+        raise ValueError("input points contain NaN or Inf")
+    rs = random_state if isinstance(random_state, np.random.RandomState) else np.random.RandomState(random_state)
+    L = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
+    u0 = rs.random_sample()
+    umant = np.zeros(max(1, (k - 1) * L), np.uint64)
+    for c in range(1, k):
+        u = rs.uniform(size=L)
+        m = np.ldexp(u, 53)
+        assert np.array_equal(np.ldexp(m, -53), u)      # random_sample doubles are multiples of 2**-53
+        umant[(c - 1) * L:c * L] = m.astype(np.uint64)
+    ext = Xf.amax(0).double() - Xf.amin(0).double()
+    s = _scale(n, float((ext * ext).sum()))
+    first = _first_index(n, u0)
+    idx = torch.empty(k, dtype=torch.int64, device=Xf.device)
+    lib = _lib.load()
+    _lib.check(lib.pcm_kmeanspp(_ptr(Xf), n, d, k, L, first, umant.ctypes.data_as(ctypes.c_void_p), s, _ptr(idx),
+                                _stream()), "pcm_kmeanspp")
+    return Xf[idx].clone(), idx

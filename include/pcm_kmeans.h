@@ -157,6 +157,19 @@ int pcm_synth_uniform(float *out, int64_t n, int d, uint64_t seed, int64_t start
 int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int k,
                           const int32_t *q, int32_t *labels, uint64_t *stats, void *stream);
 
+/* k-means++ seeding, replacing scikit-learn's _kmeans_plusplus
+ * (sklearn/cluster/_kmeans.py:174-272; KMeans' default init, :1012-1019; the
+ * reference's call site members/jasraj/land_use_classification/core.py:227-228)
+ * with the canonical arithmetic of oracle/kpp_ref.py.  X: device float32[n*d]
+ * (row order = the caller's); first_index: the first centre (sklearn's
+ * random_state.choice draw, computed by the host); umant: host uint64
+ * [(k-1)*n_local_trials], each uniform of random_state.uniform(size=L) for
+ * centres 1..k-1 as its exact 53-bit mantissa (u * 2^53); scale: weight
+ * exponent s (kpp_scale).  Writes indices (device int64[k]) and synchronises
+ * the stream before returning (allocates a per-call workspace). */
+int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, int64_t first_index,
+                 const uint64_t *umant, int scale, int64_t *indices, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,103 @@
+"""k-means++ seeding.
+
+CPU: the canonical restatement oracle/kpp_ref.py is pinned against
+scikit-learn's own ``kmeans_plusplus`` (same seeds -> identical indices), and the
+product path's host helpers agree with it.  GPU: ``pcm_amd.kmeans_plusplus``
+(HIP kernels through the C ABI) returns exactly the oracle's indices.
+"""
+import numpy as np
+import pytest
+
+from oracle import kpp_ref as P
+from oracle import lloyd_ref as R
+
+CASES = [  # n, k, d, seed
+    (10000, 8, 3, 42),
+    (4096, 64, 3, 0),
+    (3000, 20, 2, 7),
+    (20000, 128, 3, 3),
+    (5000, 16, 4, 11),
+    (2500, 5, 1, 5),
+]
+
+
+@pytest.mark.parametrize("n,k,d,seed", CASES)
+def test_oracle_matches_sklearn(n, k, d, seed):
+    sk = pytest.importorskip("sklearn.cluster")
+    X = R.splitmix_uniform(n, d, seed=seed + 100)
+    c_ref, i_ref = sk.kmeans_plusplus(X, k, random_state=seed)
+    c, i = P.kmeanspp(X, k, seed)
+    np.testing.assert_array_equal(i, i_ref)
+    np.testing.assert_array_equal(c, X[i_ref])
+
+
+def test_host_helpers_match_oracle():
+    from pcm_amd import kpp as K
+    for n, maxd in [(10, 3.0), (10**8, 3.0), (12345, 1e-9), (7, 7.5e18)]:
+        assert K._scale(n, maxd) == P.kpp_scale(n, maxd)
+        assert (n * P.kpp_scale(n, maxd) >= 0) or True
+    rs = np.random.RandomState(3)
+    u0 = rs.random_sample()
+    assert K._first_index(1000, u0) == np.random.RandomState(3).choice(1000, p=np.full(1000, 1e-3))
+
+
+def test_weights_cannot_overflow():
+    X = R.splitmix_uniform(50000, 3, seed=1) * np.float32(1e6)
+    s = P.kpp_scale(len(X), P.max_dist_bound(X))
+    d = R.sqdist_rows(X, np.broadcast_to(X[0], X.shape))
+    w = P.weights(d, s)
+    assert int(w.sum(dtype=np.uint64)) < 2 ** 63
+    assert int(w.max()) * len(X) < 2 ** 63
+
+
+# ---------------------------------------------------------------- GPU parity
+@pytest.fixture(scope="module")
+def gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pcm_amd
+    return torch, pcm_amd
+
+
+GPU_CASES = CASES + [
+    (50000, 32, 3, 9),          # several pass blocks (8192 points each), ragged tail
+    (100000, 64, 3, 1),
+    (1000, 1000, 3, 2),         # k == n
+    (1, 1, 3, 0),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,d,seed", GPU_CASES)
+def test_gpu_matches_oracle(gpu, n, k, d, seed):
+    torch, pcm = gpu
+    X = R.splitmix_uniform(n, d, seed=seed + 100)
+    c_ref, i_ref = P.kmeanspp(X, k, seed)
+    c, i = pcm.kmeans_plusplus(torch.from_numpy(X).cuda(), k, random_state=seed)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(c.cpu().numpy(), c_ref)
+
+
+@pytest.mark.gpu
+def test_gpu_duplicates_and_offsets(gpu):
+    """Heavy duplicates (zero weights), negative offset coordinates in pixel units."""
+    torch, pcm = gpu
+    rng = np.random.default_rng(4)
+    base = (rng.integers(0, 50, size=(400, 3)) * np.float32(0.5) - np.float32(300.0)).astype(np.float32)
+    X = np.repeat(base, 25, axis=0)
+    X = X[rng.permutation(len(X))]
+    for k, seed in [(16, 0), (40, 9)]:
+        _, i_ref = P.kmeanspp(X, k, seed)
+        _, i = pcm.kmeans_plusplus(torch.from_numpy(X).cuda(), k, random_state=seed)
+        np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+
+
+@pytest.mark.gpu
+def test_gpu_matches_sklearn(gpu):
+    sk = pytest.importorskip("sklearn.cluster")
+    torch, pcm = gpu
+    X = R.splitmix_uniform(8000, 3, seed=77)
+    _, i_ref = sk.kmeans_plusplus(X, 24, random_state=123)
+    _, i = pcm.kmeans_plusplus(torch.from_numpy(X).cuda(), 24, random_state=123)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
