@@ -71,13 +71,26 @@ def _norm(v: np.ndarray) -> np.ndarray:
     return np.clip((v - lo) / (hi - lo + 1e-6), 0.0, 1.0)
 
 
+def _gpu_kpp(X: np.ndarray, k: int, seed: int) -> np.ndarray:
+    import torch
+
+    from .kpp import kmeans_plusplus
+
+    with _gpu_lock:
+        C, _ = kmeans_plusplus(torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).cuda(), k,
+                               random_state=seed)
+        return C.cpu().numpy()
+
+
 def kmeans_fuse(clouds: Sequence[np.ndarray], n_clusters: int = 1024, max_iter: int = 300, tol: float = 1e-4,
-                seed: int = 1, fit: Optional[Callable] = None):
+                seed: int = 1, fit: Optional[Callable] = None, init: str = "rows"):
     """Fuse per-pair (M_i, 3) z,y,x clouds into one K-means reconstruction.
 
     Returns (layers, result) where ``result`` has labels (N,), centers (K, 3),
-    inertia, n_iter.  Init: rows ``sorted(default_rng(seed).choice(N, K))``
-    (SURVEY.md §8d); K is clipped to N.
+    inertia, n_iter.  ``init``: ``"rows"`` = rows ``sorted(default_rng(seed).choice(N, K))``
+    (SURVEY.md §8d); ``"k-means++"`` = GPU k-means++ with ``random_state=seed``
+    (scikit-learn's KMeans default, sklearn/cluster/_kmeans.py:1012-1019).
+    K is clipped to N.
     """
     clouds = [np.asarray(c, dtype=np.float64).reshape(-1, 3) for c in clouds if np.asarray(c).size]
     if not clouds:
@@ -85,8 +98,12 @@ def kmeans_fuse(clouds: Sequence[np.ndarray], n_clusters: int = 1024, max_iter: 
     X = np.concatenate(clouds).astype(np.float32)          # boundary cast
     n = X.shape[0]
     k = int(min(n_clusters, n))
-    idx = np.sort(np.random.default_rng(seed).choice(n, k, replace=False))
-    C0 = X[idx]
+    if init == "k-means++":
+        C0 = _gpu_kpp(X, k, seed)
+    elif init == "rows":
+        C0 = X[np.sort(np.random.default_rng(seed).choice(n, k, replace=False))]
+    else:
+        raise ValueError(f"init must be 'rows' or 'k-means++', got {init!r}")
     labels, centers, inertia, n_iter = (fit or _gpu_fit)(X, C0, int(max_iter), _tolerance(X, tol))
     counts = np.bincount(labels, minlength=k)
     layers = [
@@ -110,8 +127,10 @@ class HeightMapExtractor(SatellitePlugin):
     requires_image = False
 
     def __init__(self, base=None, n_clusters: int = 1024, max_iter: int = 300, tol: float = 1e-4,
-                 fit: Optional[Callable] = None):
+                 fit: Optional[Callable] = None, init: str = "rows", seed: int = 1):
         self._base = base
+        self.init = init
+        self.seed = seed
         self.n_clusters = n_clusters
         self.max_iter = max_iter
         self.tol = tol
@@ -140,7 +159,8 @@ class HeightMapExtractor(SatellitePlugin):
                       if kind == "points" and str(params.get("name", "")).endswith(CLOUD_LAYER_SUFFIX)]
             if not clouds:   # the pipeline returned only images (or an error layer): pass it through
                 return layers
-            fused, self.last_result = kmeans_fuse(clouds, self.n_clusters, self.max_iter, self.tol, fit=self._fit)
+            fused, self.last_result = kmeans_fuse(clouds, self.n_clusters, self.max_iter, self.tol, seed=self.seed,
+                                                  fit=self._fit, init=self.init)
             return layers + fused
         except Exception as e:   # reference convention: an error layer, never an exception
             import traceback

@@ -206,6 +206,21 @@ def test_plugin_gpu_matches_oracle(pcm):
     np.testing.assert_array_equal(fused[0][0].astype(np.float32), ref["centers"])
 
 
+def test_plugin_gpu_kmeanspp_init(pcm):
+    """init='k-means++' (sklearn's default): GPU seeding + GPU Lloyd = oracle seeding + oracle Lloyd."""
+    from fake_pipeline import SyntheticPairExtractor
+    from oracle import kpp_ref as P
+    plugin = pcm.HeightMapExtractor(base=SyntheticPairExtractor(n_pairs=2, shape=(80, 100)), n_clusters=32,
+                                    max_iter=40, tol=0.0, init="k-means++", seed=5)
+    layers = plugin.run("roi.kml")
+    fused = [l for l in layers if "Fused" in l[1]["name"]]
+    X = fused[1][0].astype(np.float32)
+    C0, _ = P.kmeanspp(X, 32, 5)
+    ref = R.lloyd_fit(X, C0, max_iter=40, fast=True)
+    np.testing.assert_array_equal(fused[1][1]["properties"]["cluster"], ref["labels"])
+    np.testing.assert_array_equal(fused[0][0].astype(np.float32), ref["centers"])
+
+
 def test_unpruned_full_lists(pcm):
     """Extent >= 1e18 disables pruning: every cell scans all K centres (the
     FULL path, including the previous-iteration scan over the kept centres)."""
