@@ -239,7 +239,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->prev, nstat * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->scratch_d, sizeof(double));
-    err = err ? err : hipMalloc(&e->partials, (size_t)NREP * k * (d + 1) * sizeof(unsigned long long));
+    err = err ? err : hipMalloc(&e->partials, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
     e->stats = e->stats_own;
     err = err ? err : hipMalloc(&e->held, nstat * sizeof(unsigned long long));
@@ -251,7 +251,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->bbox_out, 2 * MAXD * sizeof(double));
     err = err ? err : hipMalloc(&e->cand_stats, 3 * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->empty_idx, (size_t)k * sizeof(int));
-    err = err ? err : hipMemset(e->partials, 0, (size_t)NREP * k * (d + 1) * sizeof(unsigned long long));
+    err = err ? err : hipMemset(e->partials, 0, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMemset(e->ctrl, 0, sizeof(Ctrl));
     if (err != hipSuccess) {
         pcm_engine_destroy(e);
@@ -450,6 +450,8 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     return 0;
 }
 
+static int launch_candidates(pcm_engine *e, hipStream_t s, int gate);
+
 int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void *stream) {
     if (!e || !C0) return fail(PCM_E_ARG, "bad argument");
     if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
@@ -468,7 +470,7 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
     // previous raw statistics := 0: iteration 0 "converges" only for an empty cloud,
     // as sklearn's labels-vs-(-1) comparison does
     HIPCHK(hipMemsetAsync(e->prev, 0, ((size_t)e->k * (e->d + 1) + 1) * sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(e->partials, 0, (size_t)NREP * e->k * (e->d + 1) * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(e->partials, 0, (size_t)2 * e->k * (e->d + 1) * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->hist_changed, 0, (size_t)e->max_iter_cap * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->hist_shift, 0, (size_t)e->max_iter_cap * sizeof(double), s));
     e->ctrl_host = Ctrl{};
@@ -476,13 +478,14 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
     e->ctrl_host.tol = tol;
     HIPCHK(hipMemcpyAsync(e->ctrl, &e->ctrl_host, sizeof(Ctrl), hipMemcpyHostToDevice, s));
     e->fit_ready = true;
-    return 0;
+    // candidate lists of C0 (later iterations get theirs from k_step / the resume path)
+    return launch_candidates(e, s, 0);
 }
 
 static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_cand<D><<<(int)(e->g.ncoarse * CAND_BPC), 256, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
+        k_cand<D><<<(int)(e->g.ncoarse * CAND_BPC), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
                                                                  e->ctrl, gate);
         LAUNCHCHK();
         return 0;
@@ -569,11 +572,11 @@ static int timing_mark(pcm_engine *e, int which, hipStream_t s) {
     return 0;
 }
 
-// Candidates + k_lloyd; with fold, k_fold folds the replicas into `stats`
-// (multi-GPU: the all-reduce input); without, k_global folds them itself.
+// k_lloyd (its candidate lists were built by the previous k_step, the resume
+// path or pcm_fit_begin); with fold, k_fold copies partials[parity] into
+// `stats` (the all-reduce input) and zeroes it.
 static int iter_local_impl(pcm_engine *e, hipStream_t s, bool fold) {
     if (int rc = timing_mark(e, 0, s)) return rc;
-    if (int rc = launch_candidates(e, s, 1)) return rc;
     if (int rc = timing_mark(e, 1, s)) return rc;
     LloydArgs A = lloyd_args(e);
     return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
@@ -601,22 +604,33 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
     return iter_local_impl(e, (hipStream_t)stream, true);
 }
 
-static int iter_global_impl(pcm_engine *e, hipStream_t s, bool fold) {
-    return dispatch_d(e->d, [&](auto DD) -> int {
+// Centre update + next candidate lists.  stats_in: the all-reduced statistics
+// (multi-GPU / resume) or nullptr (single GPU: partials[parity]).  K <=
+// KSTEP_MAX: one fused k_step launch; otherwise k_global then k_cand.  The
+// relocation resume always takes k_global (it handles `resume`) + k_cand.
+static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bool resume_path) {
+    int rc = dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_global<D><<<1, 1024, 0, s>>>(fold ? e->partials : nullptr, e->stats, e->k, e->qe, e->held, e->prev, e->C,
-                                       e->Cn, e->hist_changed,
-                                       e->hist_shift,
-                                       e->ctrl);
+        if (e->k <= KSTEP_MAX && !resume_path) {
+            k_step<D><<<(int)(e->g.ncoarse * CAND_BPC + 1), CAND_TPB, (size_t)e->k * sizeof(float4), s>>>(
+                e->g, from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C,
+                e->hist_changed, e->hist_shift, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab);
+            LAUNCHCHK();
+            return 0;
+        }
+        k_global<D><<<1, 1024, 0, s>>>(from_partials ? e->partials : nullptr, e->stats, e->k, e->qe, e->held, e->prev,
+                                       e->C, e->Cn, e->hist_changed, e->hist_shift, e->ctrl);
         LAUNCHCHK();
-        return timing_mark(e, 3, s);
+        return launch_candidates(e, s, 1);
     });
+    if (rc) return rc;
+    return timing_mark(e, 3, s);
 }
 
 int pcm_iter_global(pcm_engine *e, void *stream) {
     if (!e) return fail(PCM_E_ARG, "null engine");
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
-    return iter_global_impl(e, (hipStream_t)stream, false);
+    return iter_global_impl(e, (hipStream_t)stream, false, false);
 }
 
 int pcm_timing(pcm_engine *e, int enable) {
@@ -643,7 +657,7 @@ int pcm_iterate(pcm_engine *e, int n, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     for (int i = 0; i < n; ++i) {
         if (int rc = iter_local_impl(e, s, false)) return rc;
-        if (int rc = iter_global_impl(e, s, true)) return rc;
+        if (int rc = iter_global_impl(e, s, true, false)) return rc;
     }
     return 0;
 }
@@ -744,7 +758,7 @@ int pcm_reloc_apply(pcm_engine *e, const void *records, int n_rec, void *stream)
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(e->stats, e->held, ((size_t)e->k * (e->d + 1) + 1) * sizeof(unsigned long long),
                           hipMemcpyDeviceToDevice, s));
-    return pcm_iter_global(e, stream);
+    return iter_global_impl(e, s, false, true);
 }
 
 int pcm_final(pcm_engine *e, void *stream) {
@@ -931,5 +945,12 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
         if (p) (void)hipFree(p);
     return rc;
 }
+
+#ifdef PCM_DBG_TIMING
+int pcm_debug_timing(unsigned long long *out, int nblocks) {
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_t), (size_t)nblocks * 8 * sizeof(unsigned long long)));
+    return 0;
+}
+#endif
 
 }  // extern "C"

@@ -28,7 +28,7 @@ constexpr int CAPF = 64;           // fine candidate capacity
 constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-centre ranks)
 constexpr int TPB = 256;           // assign block size
 constexpr int TILE = 8192;         // max points per tile (<= 63 per lane per flush)
-constexpr int NREP = 8;            // replicas of the global partials
+constexpr int KSTEP_MAX = 2048;    // k_step keeps the K new centres in LDS (<= 32 KB)
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int QBITS = 25;
 // Pruning margins (see DESIGN.md "Exactness of pruning").
@@ -55,6 +55,8 @@ struct Ctrl {
     unsigned long long neq_saved;   // stat words changed at a halted iteration (used on resume)
     unsigned long long last_changed;
     double last_shift;
+    unsigned int step_done;         // k_step: blocks finished (the last one advances `iter`)
+    unsigned int pad1;
 };
 
 // Fixed-point exponents q_a (identical on every rank).
@@ -286,16 +288,40 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
 //     not dominate, in ascending centroid order (the scan's tie rule); the count
 //     goes to fc_cnt[cell] (FULL = more than CAPF, or pruning disabled).
 #ifndef PCM_CAND_BPC
-#define PCM_CAND_BPC 2
+#define PCM_CAND_BPC 1
 #endif
 constexpr int CAND_BPC = PCM_CAND_BPC;   // blocks per coarse cell
+#ifndef PCM_CAND_TPB
+#define PCM_CAND_TPB 256
+#endif
+constexpr int CAND_TPB = PCM_CAND_TPB;   // threads per candidate block (one child cell per wave at a time)
 constexpr int CAND_KBITS = 4096;         // bitmap capacity (larger K: direct ballot compaction)
 
+#ifdef PCM_DBG_TIMING
+__device__ unsigned long long g_dbg_t[8192][8];
+#define DBG_T(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define DBG_T(k) do { } while (0)
+#endif
+
+// Wave-wide minimum through DPP (row_shr 1/2/4/8 scan, then row_bcast 15/31;
+// lane 63 ends with the minimum).  The whole wave must be active.  Used only to
+// pick pruning references, where any candidate is correct (callers clamp).
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    const int id = -1;   // 0xFFFFFFFF: the identity of unsigned min
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x142, 0xA, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x143, 0xC, 0xF, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// C: the K centres, in global memory (k_cand) or in LDS (k_step).
 template <int D>
-__global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__ C, int K,
-                                              uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                              int32_t *__restrict__ fc_lab, const Ctrl *__restrict__ ctrl, int gate) {
-    if (gate && gated(ctrl)) return;
+__device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K, uint32_t *__restrict__ fc_cnt,
+                                          float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab) {
     const long long I = blockIdx.x / CAND_BPC;
     const int bsub = blockIdx.x % CAND_BPC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -303,7 +329,6 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
     __shared__ int pidx[CAPC];
     __shared__ unsigned long long kbits[CAND_KBITS / 64];
     __shared__ unsigned long long rkey;
-    __shared__ uint32_t wkey[4];
     __shared__ uint32_t s_mp;
     int ci[MAXD];
     decode(I, g.GC, D, ci);
@@ -323,22 +348,28 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
         const bool bitmap = K <= CAND_KBITS;
         if (tid == 0) rkey = ~0ull;
         if (bitmap)
-            for (int w = tid; w < CAND_KBITS / 64; w += 256) kbits[w] = 0ull;
+            for (int w = tid; w < CAND_KBITS / 64; w += CAND_TPB) kbits[w] = 0ull;
         __syncthreads();
-        unsigned long long best = ~0ull;
-        for (int j = tid; j < K; j += 256) {
-            // key: fp64 bits of a non-negative distance (monotonic), low 21 bits -> index
-            const double m = maxdist<D>(blo, bhi, C[j]);
-            const unsigned long long key = (__double_as_longlong(m) & ~0x1FFFFFull) | (unsigned long long)j;
-            best = key < best ? key : best;
+        // reference key: fp32 bits of the max distance (any centre is a valid
+        // reference; the key only ranks them) with the low 11 bits replaced by
+        // j's wave-local rank -> per-wave DPP minimum, then one LDS atomic per wave
+        uint32_t best = ~0u;
+        int bjj = 0;
+        for (int j = tid; j < K; j += CAND_TPB) {
+            const float m = (float)maxdist<D>(blo, bhi, C[j]);
+            if (__float_as_uint(m) < best) { best = __float_as_uint(m); bjj = j; }
         }
-        atomicMin(&rkey, best);
+        const uint32_t wbest = wave_min_u32(best);
+        const unsigned long long bal = __ballot(best == wbest);
+        if (lane == (int)(__ffsll((long long)bal) - 1)) atomicMin(&rkey, ((unsigned long long)wbest << 32) | (unsigned)bjj);
         __syncthreads();
-        const float4 r = C[(int)(rkey & 0x1FFFFFull)];
+        DBG_T(4);
+        const float4 r = C[(int)min((unsigned long long)(K - 1), rkey & 0xFFFFFFFFull)];
         if (bitmap) {
-            for (int j = tid; j < K; j += 256)
+            for (int j = tid; j < K; j += CAND_TPB)
                 if (!prunable<D>(blo, bhi, C[j], r)) atomicOr(&kbits[j >> 6], 1ull << (j & 63));
             __syncthreads();
+            DBG_T(5);
             if (wv == 0) {
                 uint32_t total = 0;
                 for (int w = 0; w < (K + 63) / 64; ++w) {
@@ -354,10 +385,10 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
                 if (lane == 0) s_mp = total <= (uint32_t)CAPC ? total : FULL;
             }
         } else {
-            // large K: ordered compaction by ballots (one barrier pair per 256 centres)
-            __shared__ uint32_t wcnt[4];
+            // large K: ordered compaction by ballots (one barrier pair per CAND_TPB centres)
+            __shared__ uint32_t wcnt[CAND_TPB / 64];
             uint32_t total = 0;
-            for (int base = 0; base < K; base += 256) {
+            for (int base = 0; base < K; base += CAND_TPB) {
                 const int j = base + tid;
                 const bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r);
                 const unsigned long long bal = __ballot(keep);
@@ -370,7 +401,7 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
                     prec[pos] = C[j];
                     pidx[pos] = j;
                 }
-                total += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+                for (int w = 0; w < CAND_TPB / 64; ++w) total += wcnt[w];
                 __syncthreads();
             }
             if (tid == 0) s_mp = total <= (uint32_t)CAPC ? total : FULL;
@@ -382,6 +413,7 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
     uint32_t mp = s_mp;
     const bool pfull = (mp == FULL);
     if (pfull) mp = (uint32_t)K;
+    DBG_T(1);
 #ifdef PCM_ABL_COARSEONLY
     if (mp != 12345u) return;
 #endif
@@ -389,7 +421,7 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
     // ---- 2. one wave per child cell (F = 4 children per axis)
     auto child = [&](auto PFc) {
         constexpr bool PF = decltype(PFc)::value;
-        for (int ch = bsub * cpb + wv; ch < min(nchild, (bsub + 1) * cpb); ch += 4) {
+        for (int ch = bsub * cpb + wv; ch < min(nchild, (bsub + 1) * cpb); ch += CAND_TPB / 64) {
             int f[MAXD];
             bool inside = true;
 #pragma unroll
@@ -429,7 +461,6 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
                     if (ob < bd || (ob == bd && ol < bl)) { bd = ob; bl = ol; }
                 }
             } else {   // key = distance bits (low byte dropped) | list position (< CAPC)
-                if (lane == 0) wkey[wv] = ~0u;
                 uint32_t best = ~0u;
                 for (uint32_t l = lane; l < mp; l += 64) {
                     const float4 c = prec[l];
@@ -442,8 +473,8 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
                     const uint32_t key = (__float_as_uint(dsum) & 0xFFFFFF00u) | l;
                     best = key < best ? key : best;
                 }
-                atomicMin(&wkey[wv], best);
-                bl = (int)(wkey[wv] & 0xFFu);
+                bl = (int)(wave_min_u32(best) & 0xFFu);
+                if (bl >= (int)mp) bl = 0;
             }
             const float4 r = PF ? C[bl] : prec[bl];
             uint32_t total = 0;
@@ -467,6 +498,15 @@ __global__ __launch_bounds__(256) void k_cand(Grid g, const float4 *__restrict__
     };
     if (pfull) child(std::integral_constant<bool, true>{});
     else child(std::integral_constant<bool, false>{});
+    DBG_T(2);
+}
+
+template <int D>
+__global__ __launch_bounds__(CAND_TPB) void k_cand(Grid g, const float4 *__restrict__ C, int K,
+                                              uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
+                                              int32_t *__restrict__ fc_lab, const Ctrl *__restrict__ ctrl, int gate) {
+    if (gate && gated(ctrl)) return;
+    cand_body<D>(g, C, K, fc_cnt, fc_rec, fc_lab);
 }
 
 // ------------------------------------------------------------------ assign
@@ -517,17 +557,23 @@ template <> struct RawLab<int32_t> {
     u32x4 w;
 };
 
+// Cache policy of the point stream (0 = default; 2 = NT measured 22% slower:
+// 349 vs 282 us per launch, and no gain in the other kernels).
+#ifndef PCM_XLOAD_CPOL
+#define PCM_XLOAD_CPOL 0
+#endif
+
 // off_pt = index of the lane's first point; one descriptor for the whole AoS array.
 template <typename T, int D>
 __device__ __forceinline__ void load_x(Raw<T, D> &r, rsrc_t rs, unsigned off_pt) {
     constexpr int NW = Raw<T, D>::NW;
     const unsigned boff = off_pt * (unsigned)(D * sizeof(T));
     for (int k = 0; k + 4 <= NW; k += 4) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff + 4u * k, 0, 0);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff + 4u * k, 0, PCM_XLOAD_CPOL);
         r.w[k] = v[0]; r.w[k + 1] = v[1]; r.w[k + 2] = v[2]; r.w[k + 3] = v[3];
     }
     if (NW % 4 == 2) {
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, boff + 4u * (NW - 2), 0, 0);
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, boff + 4u * (NW - 2), 0, PCM_XLOAD_CPOL);
         r.w[NW - 2] = v[0]; r.w[NW - 1] = v[1];
     }
 }
@@ -594,7 +640,7 @@ struct LloydArgs {
     const float4 *C;                // all centres (FULL cells)
     int K;
     int q[MAXD];
-    unsigned long long *partials;   // [NREP][K][D+1]
+    unsigned long long *partials;   // [2][K][D+1]: iteration parity halves
     const Ctrl *ctrl;
 };
 
@@ -799,7 +845,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     LOAD_X(xb, item_off(1));
     __syncthreads();
 
-    unsigned long long *prep = A.partials + (size_t)(blockIdx.x % NREP) * A.K * (D + 1);
+    unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.K * (D + 1);
     int par = 0;
 
     auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx) -> bool {
@@ -908,26 +954,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     }
 }
 
-// stats[j*(D+1)+q] = sum over replicas; partials := 0; stats[K*(D+1)] = 0
+// stats := partials[parity] (the all-reduce input); partials[parity] := 0; stats[K*(D+1)] = 0
 template <int D>
 __global__ __launch_bounds__(256) void k_fold(unsigned long long *__restrict__ partials, int K,
                                               unsigned long long *__restrict__ stats, Ctrl *__restrict__ ctrl) {
     if (gated(ctrl)) return;
     const int n = K * (D + 1);
+    unsigned long long *src = partials + (size_t)(ctrl->iter & 1u) * n;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
-        unsigned long long s = 0;
-        for (int r = 0; r < NREP; ++r) {
-            s += partials[(size_t)r * n + i];
-            partials[(size_t)r * n + i] = 0ull;
-        }
-        stats[i] = s;
+        stats[i] = src[i];
+        src[i] = 0ull;
     }
     if (i == n) stats[n] = 0ull;
 }
 
-// Single block of 1024 threads.  Optionally first folds the NREP replicas of
-// the partials into `stats` (single-GPU path: no all-reduce in between).  Then
+// Single block of 1024 threads.  Optionally first folds partials[parity] into
+// `stats` (single-GPU path: no all-reduce in between).  Then
 // reads the (all-reduced) statistics, halts for relocation when a cluster is
 // empty (unless resuming), otherwise averages, computes the shift with the
 // fixed reduction tree (per-thread sums over j = tid + 1024 r, then the halving
@@ -952,9 +995,9 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
     if (tid == 0) { cnt_empty = 0; neq_s = 0ull; }
     __syncthreads();
     const uint32_t resume = ctrl->resume;
-    // Thread tid owns centroids j = tid + 1024 r: every load of a row (its NREP
-    // replicas, the previous statistics) is issued before any is consumed, so a
-    // pass costs one memory round trip.
+    // Thread tid owns centroids j = tid + 1024 r: every load of a row (and of
+    // the previous statistics) is issued before any is consumed, so a pass
+    // costs one memory round trip.
     // Convergence (sklearn: labels equal, _kmeans.py:717-723): the raw statistics
     // of this iteration (before any relocation move) equal the previous ones.
     unsigned long long neq = 0, bmax = 0;
@@ -964,25 +1007,14 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
         unsigned long long row[D + 1], pv[D + 1];
         const size_t o = (size_t)j * (D + 1);
         if (partials) {
-            unsigned long long part[NREP][D + 1];
+            unsigned long long *src = partials + (size_t)(ctrl->iter & 1u) * n;
 #pragma unroll
-            for (int r = 0; r < NREP; ++r)
-#pragma unroll
-                for (int a = 0; a <= D; ++a) part[r][a] = partials[(size_t)r * n + o + a];
-#pragma unroll
-            for (int a = 0; a <= D; ++a) pv[a] = prev[o + a];
+            for (int a = 0; a <= D; ++a) { row[a] = src[o + a]; pv[a] = prev[o + a]; }
 #pragma unroll
             for (int a = 0; a <= D; ++a) {
-                row[a] = 0ull;
-#pragma unroll
-                for (int r = 0; r < NREP; ++r) row[a] += part[r][a];
+                src[o + a] = 0ull;
+                stats[o + a] = row[a];
             }
-#pragma unroll
-            for (int r = 0; r < NREP; ++r)
-#pragma unroll
-                for (int a = 0; a <= D; ++a) partials[(size_t)r * n + o + a] = 0ull;
-#pragma unroll
-            for (int a = 0; a <= D; ++a) stats[o + a] = row[a];
         } else {
 #pragma unroll
             for (int a = 0; a <= D; ++a) { row[a] = stats[o + a]; pv[a] = prev[o + a]; }
@@ -1110,6 +1142,146 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
             ctrl->done = done;
         }
     }
+}
+
+// ------------------------------------------------------------------ fused update + candidates
+// One launch per iteration for the centre update AND the next candidate lists
+// (k_global + k_cand fused; K <= KSTEP_MAX).  Every block recomputes the K new
+// centres from the integer statistics into LDS -- deterministic, so all blocks
+// agree bit for bit -- and builds its candidate lists from them; one extra
+// block (the last) does only the bookkeeping of k_global (statistics-equality test, fixed-tree shift,
+// history, flags, C := new centres) and zeroes the other parity half of the
+// partials.  An empty cluster halts (that block snapshots the statistics; the
+// host relocates, then k_global + k_cand resume).  src: the all-reduced stats
+// (multi-GPU) or nullptr = partials[parity] (single GPU).
+template <int D>
+__global__ __launch_bounds__(CAND_TPB) void k_step(Grid g, const unsigned long long *__restrict__ stats_in,
+                                              unsigned long long *__restrict__ partials, int K, QExp qe,
+                                              unsigned long long *__restrict__ held,
+                                              unsigned long long *__restrict__ prev, float4 *__restrict__ C,
+                                              unsigned long long *__restrict__ hist_changed,
+                                              double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl,
+                                              uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
+                                              int32_t *__restrict__ fc_lab) {
+    if (gated(ctrl)) return;
+    DBG_T(0);
+    extern __shared__ __attribute__((aligned(16))) float4 cn[];   // [K]
+    __shared__ unsigned s_empty;
+    __shared__ unsigned long long s_neq;
+    __shared__ double ssum[1024];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int n = K * (D + 1);
+    const unsigned par = ctrl->iter & 1u;
+    const unsigned long long *src = stats_in ? stats_in : partials + (size_t)par * n;
+    const bool b0 = blockIdx.x == gridDim.x - 1;   // the bookkeeping block (builds no candidate lists)
+    if (tid == 0) { s_empty = 0; s_neq = 0ull; }
+    __syncthreads();
+    unsigned ne = 0;
+    unsigned long long neq = 0;
+    for (int j = tid; j < K; j += CAND_TPB) {
+        unsigned long long row[D + 1];
+#pragma unroll
+        for (int a = 0; a <= D; ++a) row[a] = src[(size_t)j * (D + 1) + a];
+        const unsigned long long c = row[D];
+        float out[4] = {0.f, 0.f, 0.f, 0.f};
+        if (c > 0) {
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                const double m = ((double)(long long)row[a] * __builtin_ldexp(1.0, -qe.q[a])) / (double)c;
+                out[a] = (float)m;
+            }
+        } else {
+            ++ne;
+        }
+        cn[j] = make_float4(out[0], out[1], out[2], out[3]);
+        if (b0) {   // convergence (sklearn: labels equal): raw statistics equal the previous ones
+#pragma unroll
+            for (int a = 0; a <= D; ++a) {
+                neq += (row[a] != prev[(size_t)j * (D + 1) + a]) ? 1ull : 0ull;
+                prev[(size_t)j * (D + 1) + a] = row[a];
+            }
+        }
+    }
+    if (ne) atomicAdd(&s_empty, ne);
+    if (neq) atomicAdd(&s_neq, neq);
+    __syncthreads();
+    if (b0 && !stats_in)   // the next iteration accumulates into the other half
+        for (int i = tid; i < n; i += CAND_TPB) partials[(size_t)(par ^ 1u) * n + i] = 0ull;
+    if (s_empty > 0) {
+        if (b0) {
+            for (int i = tid; i < n; i += CAND_TPB) held[i] = src[i];
+            if (tid == 0) {
+                held[n] = 0ull;
+                ctrl->halt = 1u;
+                ctrl->n_empty = s_empty;
+                ctrl->neq_saved = s_neq;
+            }
+        }
+        return;
+    }
+    if (b0) {
+        // shift with the fixed tree of k_global: lane L (0..1023) sums j = L + 1024 r
+        // sequentially; thread tid plays lanes tid + CAND_TPB u; then halving 512..1
+        for (int u = 0; u < 1024 / CAND_TPB; ++u) {
+            const int L = tid + CAND_TPB * u;
+            double acc = 0.0;
+            for (int j = L; j < K; j += 1024) {
+                const float4 a4 = cn[j], b4 = C[j];
+                double sh = 0.0;
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    const double dd = (double)comp(a4, a) - (double)comp(b4, a);
+                    const double sq = dd * dd;
+                    sh = (a == 0) ? sq : sh + sq;
+                }
+                acc = acc + sh;
+            }
+            ssum[L] = acc;
+        }
+        __syncthreads();
+        for (int st = 512; st >= 1; st >>= 1) {
+            for (int L = tid; L < st; L += CAND_TPB) ssum[L] = ssum[L] + ssum[L + st];
+            __syncthreads();
+        }
+        for (int j = tid; j < K; j += CAND_TPB) C[j] = cn[j];
+        if (tid == 0) {
+            const uint32_t it = ctrl->iter;
+            if (it < ctrl->max_iter) {
+                hist_changed[it] = s_neq;
+                hist_shift[it] = ssum[0];
+            }
+            __hip_atomic_store(&ctrl->last_changed, s_neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctrl->last_shift, ssum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    DBG_T(3);
+    if (!b0) cand_body<D>(g, cn, K, fc_cnt, fc_rec, fc_lab);
+    // Every block has read ctrl->iter (parity) before any block can observe the
+    // final count, so only the last block advances the iteration and flags.
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        const unsigned prior = atomicAdd(&ctrl->step_done, 1u);
+        if (prior == gridDim.x - 1) {
+            __threadfence();
+            const unsigned long long changed =
+                __hip_atomic_load(&ctrl->last_changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double shift = __hip_atomic_load(&ctrl->last_shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t it = ctrl->iter;
+            ctrl->step_done = 0u;
+            ctrl->resume = 0u;
+            uint32_t done = 0;
+            if (changed == 0ull) done = 1u;
+            else if (shift <= ctrl->tol) done = 2u;
+#if defined(PCM_ABL_NOHALT)
+            done = 0u;
+#endif
+            if (!done && it + 1 >= ctrl->max_iter) done = 3u;
+            ctrl->done = done;
+            ctrl->iter = it + 1;
+        }
+    }
+    (void)lane;
 }
 
 // ------------------------------------------------------------------ relocation

@@ -73,8 +73,12 @@ def prepare(engine, X, group=None):
     return q, n_total
 
 
-def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8):
-    """Iteration phase on a prepared engine.  Returns (status, relocations)."""
+def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False):
+    """Iteration phase on a prepared engine.  Returns (status, relocations).
+
+    One process: ``pcm_iterate`` (k_lloyd + fused k_step per iteration).  Several
+    (or ``split``): ``iter_local`` (k_lloyd + k_fold) -> all-reduce of the
+    statistics (only when world > 1) -> ``iter_global`` (k_step on them)."""
     import torch.distributed as dist
     world, _ = _world(group)
     engine.begin(C0, tol, max_iter)
@@ -82,12 +86,13 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8):
     it = 0
     while True:
         n_enq = max(1, min(chunk, max_iter - it))
-        if world == 1:
+        if world == 1 and not split:
             engine.iterate(n_enq)
         else:
             for _ in range(n_enq):
                 engine.iter_local()
-                dist.all_reduce(engine.stats, group=group)
+                if world > 1:
+                    dist.all_reduce(engine.stats, group=group)
                 engine.iter_global()
         st = engine.status()
         if st["halt"]:
@@ -118,7 +123,7 @@ def finish(engine, group=None):
 
 
 def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=None, chunk: int = 8,
-              engine=None) -> LloydResult:
+              engine=None, split: bool = False) -> LloydResult:
     """Fit K-means (Lloyd) to this rank's shard ``X`` (N_local, D) from ``centers_init`` (K, D).
 
     ``tol`` is the absolute centre-shift tolerance (sklearn's ``_tolerance``
@@ -129,7 +134,7 @@ def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=N
         from .engine import Engine
         engine = Engine(X.shape[1], centers_init.shape[0], X.dtype, max_iter=max_iter)
     prepare(engine, X, group)
-    st, relocs = run(engine, centers_init, max_iter, tol, group, chunk)
+    st, relocs = run(engine, centers_init, max_iter, tol, group, chunk, split)
     labels, centers, inertia = finish(engine, group)
     ch, sh = engine.history(int(st["iter"]))
     return LloydResult(labels=labels, centers=centers, inertia=inertia, n_iter=int(st["iter"]),

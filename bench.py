@@ -207,8 +207,7 @@ def main():
                          "kernel": "k_lloyd<float,3>",
                          "algorithmic_bytes_per_point": bytes_pt,
                          "avg_launch_ms": assign_ms},
-            "breakdown_ms_per_iter": {"assign": assign_ms, "candidates": tm["candidates_ms"],
-                                      "fold_global": tm["tail_ms"]},
+            "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"]},
             "candidates": cand,
             "layout_ms": layout_ms,
         }

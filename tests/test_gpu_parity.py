@@ -206,6 +206,21 @@ def test_plugin_gpu_matches_oracle(pcm):
     np.testing.assert_array_equal(fused[0][0].astype(np.float32), ref["centers"])
 
 
+@pytest.mark.parametrize("name", ["cfg1_n10k_k8", "n4096_k64", "empty_reloc", "d4_fp16"])
+def test_split_call_sequence(pcm, name):
+    """The multi-GPU call sequence (iter_local -> [all-reduce] -> iter_global: k_fold +
+    k_step on `stats`) on one GPU gives the same fit as pcm_iterate and the oracle."""
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    X, C0 = g["X"], g["C0"]
+    ref = R.lloyd_fit(X, C0, max_iter=300, tol=0.0, fast=True)
+    dt = torch.float16 if X.dtype == np.float16 else torch.float32
+    res = pcm.lloyd_fit(torch.from_numpy(np.ascontiguousarray(X)).to("cuda", dt),
+                        torch.from_numpy(np.ascontiguousarray(C0, dtype=np.float32)).cuda(), max_iter=300,
+                        tol=0.0, chunk=3, split=True)
+    torch.cuda.synchronize()
+    assert_same(res, ref, name)
+
+
 def test_plugin_gpu_kmeanspp_init(pcm):
     """init='k-means++' (sklearn's default): GPU seeding + GPU Lloyd = oracle seeding + oracle Lloyd."""
     from fake_pipeline import SyntheticPairExtractor
