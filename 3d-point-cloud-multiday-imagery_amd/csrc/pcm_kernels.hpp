@@ -618,15 +618,19 @@ __device__ __forceinline__ void store_l4(rsrc_t rs, unsigned off, const int (&l)
 }
 
 #ifndef PCM_LSLOT
-#define PCM_LSLOT 8
+#define PCM_LSLOT 16
 #endif
 constexpr int LSLOT = PCM_LSLOT;
 
-// Lane-minor accumulator words: word (slot, a) of thread tid at (slot*(D+1)+a)*TPB + tid,
-// so a wave's ds_add_u32 hits 32 distinct banks per half-wave whatever the slots.
+// Lane-minor accumulator words shared by threads tid and tid + 128 (different
+// waves, so an instruction never hits one word twice): word (slot, a) of column
+// c = tid & 127 at (slot*(D+1)+a)*128 + c -- a wave's ds_add_u32 hits 32 distinct
+// banks per half-wave whatever the slots.  A word sums <= 2 x 32 points of
+// |xq| < 2^25 per tile: < 2^31, exact in int32.
+constexpr int AW = 128;
 template <int D> struct AccL {
     static constexpr int rows = (LSLOT + 1) * (D + 1);   // + junk slot
-    static constexpr int words = TPB * rows;
+    static constexpr int words = AW * rows;
 };
 
 struct LloydArgs {
@@ -728,7 +732,7 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, double *i
 // Per tile (cell): the candidate list (ascending centroid index, so the
 // strict-'<' scan keeps the lowest index on ties, _k_means_lloyd.pyx:205-213)
 // in LDS; a winner at list position j < LSLOT is summed into the thread's
-// private LDS words of slot j (ds_add_u32, lane-minor: conflict-free);
+// LDS words of slot j (ds_add_u32, lane-minor: conflict-free);
 // positions >= LSLOT (lists longer than LSLOT) use global int64 atomics.
 // Out-of-tile lanes of a partial round add into a junk slot (never read).
 // Persistent blocks walk tiles blockIdx.x, +gridDim.x, ...; the loads of the
@@ -787,7 +791,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     };
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     for (int e = tid; e < AccL<D>::words; e += TPB) acc[e] = 0u;
-    uint32_t *const myacc = acc + tid;
+    uint32_t *const myacc = acc + (tid & (AW - 1));
 
     // Candidate list of tile hh into LDS half sp: scalar loads, 4 records per
     // chunk, written by lanes 0-3 (uniform cell -> SMEM, no vector loads).
@@ -883,9 +887,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
 #else
         for (int e = 0; e < 4; ++e) {
 #endif
-            uint32_t *ap = myacc + sl[e] * ((D + 1) * TPB);
-            for (int a = 0; a < D; ++a) atomicAdd(ap + a * TPB, (uint32_t)fixed_i(x[e][a], A.q[a]));
-            atomicAdd(ap + D * TPB, 1u);
+            uint32_t *ap = myacc + sl[e] * ((D + 1) * AW);
+            for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
+            atomicAdd(ap + D * AW, 1u);
         }
         if (over) {   // list positions >= LSLOT (long lists only)
             for (int e = 0; e < 4; ++e) {
@@ -911,16 +915,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
             const int nslots = h.mm < LSLOT ? h.mm : LSLOT;
 #endif
             const int npairs = nslots * (D + 1);
-            // 16 threads per (slot, a) word, each summing 16 threads' words
+            // 16 threads per (slot, a) row, each summing AW/16 of its words
             for (int p0 = 0; p0 < npairs; p0 += TPB / 16) {
                 const int pi = p0 + tid / 16, sub = tid & 15;
                 long long sacc = 0;
                 if (pi < npairs) {
                     const bool cnt = (pi % (D + 1) == D);
-                    uint32_t *row = acc + pi * TPB;
-                    for (int k = 0; k < TPB / 16; ++k) {
+                    uint32_t *row = acc + pi * AW;
+                    for (int k = 0; k < AW / 16; ++k) {
                         uint32_t *ap = row + sub + 16 * k;
-                        // per-thread sums are exact int32 (<= 32 points of |xq| < 2^25 per tile)
                         sacc += cnt ? (long long)*ap : (long long)(int32_t)*ap;
                         *ap = 0u;
                     }
