@@ -485,7 +485,7 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
 static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_cand<D><<<(int)(e->g.ncoarse * CAND_BPC), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
+        k_cand<D><<<(int)(e->g.ncoarse * cand_bpc<D>()), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
                                                                  e->ctrl, gate);
         LAUNCHCHK();
         return 0;
@@ -612,7 +612,7 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
     int rc = dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
         if (e->k <= KSTEP_MAX && !resume_path) {
-            k_step<D><<<(int)(e->g.ncoarse * CAND_BPC + 1), CAND_TPB, (size_t)e->k * sizeof(float4), s>>>(
+            k_step<D><<<(int)(e->g.ncoarse * cand_bpc<D>() + 1), CAND_TPB, (size_t)e->k * sizeof(float4), s>>>(
                 e->g, from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C,
                 e->hist_changed, e->hist_shift, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab);
             LAUNCHCHK();

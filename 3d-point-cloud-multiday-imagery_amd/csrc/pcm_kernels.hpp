@@ -290,7 +290,10 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
 #ifndef PCM_CAND_BPC
 #define PCM_CAND_BPC 1
 #endif
-constexpr int CAND_BPC = PCM_CAND_BPC;   // blocks per coarse cell
+constexpr int CAND_BPC = PCM_CAND_BPC;   // blocks per coarse cell (D <= 3)
+// D = 4: a coarse cell has 4^4 = 256 fine cells and a longer coarse list
+template <int D> constexpr int cand_bpc() { return D >= 4 ? 16 : CAND_BPC; }
+template <int D> constexpr int cand_capc() { return D >= 4 ? 1024 : CAPC; }
 #ifndef PCM_CAND_TPB
 #define PCM_CAND_TPB 256
 #endif
@@ -322,11 +325,12 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 template <int D>
 __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K, uint32_t *__restrict__ fc_cnt,
                                           float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab) {
-    const long long I = blockIdx.x / CAND_BPC;
-    const int bsub = blockIdx.x % CAND_BPC;
+    constexpr int BPC = cand_bpc<D>(), CAP = cand_capc<D>();
+    const long long I = blockIdx.x / BPC;
+    const int bsub = blockIdx.x % BPC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    __shared__ float4 prec[CAPC];
-    __shared__ int pidx[CAPC];
+    __shared__ float4 prec[CAP];
+    __shared__ int pidx[CAP];
     __shared__ unsigned long long kbits[CAND_KBITS / 64];
     __shared__ unsigned long long rkey;
     __shared__ uint32_t s_mp;
@@ -334,7 +338,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     decode(I, g.GC, D, ci);
     int nchild = 1;
     for (int a = 0; a < D; ++a) nchild *= 4;
-    const int cpb = (nchild + CAND_BPC - 1) / CAND_BPC;
+    const int cpb = (nchild + BPC - 1) / BPC;
 
     // ---- 1. coarse list
     if (g.prune) {
@@ -376,13 +380,13 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                     const unsigned long long word = kbits[w];
                     const uint32_t pos = total + __popcll(word & ((1ull << lane) - 1ull));
                     const int j = w * 64 + lane;
-                    if (((word >> lane) & 1ull) && pos < (uint32_t)CAPC) {
+                    if (((word >> lane) & 1ull) && pos < (uint32_t)CAP) {
                         prec[pos] = C[j];
                         pidx[pos] = j;
                     }
                     total += __popcll(word);
                 }
-                if (lane == 0) s_mp = total <= (uint32_t)CAPC ? total : FULL;
+                if (lane == 0) s_mp = total <= (uint32_t)CAP ? total : FULL;
             }
         } else {
             // large K: ordered compaction by ballots (one barrier pair per CAND_TPB centres)
@@ -397,14 +401,14 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                 uint32_t woff = 0;
                 for (int w = 0; w < wv; ++w) woff += wcnt[w];
                 const uint32_t pos = total + woff + __popcll(bal & ((1ull << lane) - 1ull));
-                if (keep && pos < (uint32_t)CAPC) {
+                if (keep && pos < (uint32_t)CAP) {
                     prec[pos] = C[j];
                     pidx[pos] = j;
                 }
                 for (int w = 0; w < CAND_TPB / 64; ++w) total += wcnt[w];
                 __syncthreads();
             }
-            if (tid == 0) s_mp = total <= (uint32_t)CAPC ? total : FULL;
+            if (tid == 0) s_mp = total <= (uint32_t)CAP ? total : FULL;
         }
     } else if (tid == 0) {
         s_mp = FULL;
@@ -460,7 +464,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                     const int ol = __shfl_xor(bl, sft);
                     if (ob < bd || (ob == bd && ol < bl)) { bd = ob; bl = ol; }
                 }
-            } else {   // key = distance bits (low byte dropped) | list position (< CAPC)
+            } else {   // key = distance bits (low bits dropped) | list position (< CAP)
                 uint32_t best = ~0u;
                 for (uint32_t l = lane; l < mp; l += 64) {
                     const float4 c = prec[l];
@@ -470,10 +474,10 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                         const float dd = ctr[a] - comp(c, a);
                         dsum += dd * dd;
                     }
-                    const uint32_t key = (__float_as_uint(dsum) & 0xFFFFFF00u) | l;
+                    const uint32_t key = (__float_as_uint(dsum) & (CAP > 256 ? 0xFFFFFC00u : 0xFFFFFF00u)) | l;
                     best = key < best ? key : best;
                 }
-                bl = (int)(wave_min_u32(best) & 0xFFu);
+                bl = (int)(wave_min_u32(best) & (CAP > 256 ? 0x3FFu : 0xFFu));
                 if (bl >= (int)mp) bl = 0;
             }
             const float4 r = PF ? C[bl] : prec[bl];
