@@ -8,6 +8,7 @@ Public API
 ----------
 lloyd_fit(X, centers_init, max_iter, tol, group=None)  -> LloydResult
 kmeans_plusplus(X, n_clusters, random_state=...)       -> (centers, indices), GPU k-means++
+assemble_cloud(disparity, validity, max_disp=288)      -> per-pair (z,y,x) cloud + height property (GPU)
 kmeans_fuse(clouds, n_clusters, ...)                   -> napari layer tuples
 HeightMapExtractor                                     -> SatellitePlugin drop-in
 Engine                                                 -> the C-ABI engine wrapper
@@ -16,7 +17,7 @@ from .fixed import QBITS, fixed_q  # noqa: F401
 from .lloyd import LloydResult, lloyd_fit  # noqa: F401
 
 __all__ = ["lloyd_fit", "LloydResult", "fixed_q", "QBITS", "Engine", "kmeans_fuse", "HeightMapExtractor",
-           "build_library", "kmeans_plusplus"]
+           "build_library", "kmeans_plusplus", "assemble_cloud"]
 
 
 def __getattr__(name):
@@ -27,6 +28,9 @@ def __getattr__(name):
     if name in ("kmeans_fuse", "HeightMapExtractor", "PREFIX"):
         from . import plugin
         return getattr(plugin, name)
+    if name == "assemble_cloud":
+        from .cloud import assemble_cloud
+        return assemble_cloud
     if name == "kmeans_plusplus":
         from .kpp import kmeans_plusplus
         return kmeans_plusplus

@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 SO_PATH = os.environ.get("PCM_SO") or os.path.join(PKG_DIR, "libpcmkm.so")
 SOURCES = [os.path.join(PKG_DIR, "csrc", "pcm_engine.hip"), os.path.join(PKG_DIR, "csrc", "pcm_kernels.hpp"),
-           os.path.join(PKG_DIR, "csrc", "pcm_kpp.hpp"),
+           os.path.join(PKG_DIR, "csrc", "pcm_kpp.hpp"), os.path.join(PKG_DIR, "csrc", "pcm_cloud.hpp"),
            os.path.join(REPO_DIR, "include", "pcm_kmeans.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
@@ -26,7 +26,7 @@ EXPORTS = [
     "pcm_layout_build", "pcm_fit_begin", "pcm_iter_local", "pcm_iter_global", "pcm_iterate", "pcm_stats_ptr",
     "pcm_bind_stats", "pcm_reloc_candidates", "pcm_reloc_apply", "pcm_final", "pcm_labels", "pcm_get_centers",
     "pcm_history", "pcm_read_status", "pcm_layout_info", "pcm_candidate_stats", "pcm_synth_uniform",
-    "pcm_assign_bruteforce", "pcm_timing", "pcm_timing_read", "pcm_synth_rows", "pcm_kmeanspp",
+    "pcm_assign_bruteforce", "pcm_timing", "pcm_timing_read", "pcm_synth_rows", "pcm_kmeanspp", "pcm_cloud_assemble",
 ]
 
 _lock = threading.Lock()
@@ -92,6 +92,7 @@ def _declare(lib):
         "pcm_timing_read": ([P, P, ctypes.POINTER(I)], I),
         "pcm_synth_rows": ([P, P, I64, I, ctypes.c_uint64, P], I),
         "pcm_kmeanspp": ([P, I64, I, I, I, I64, P, I, P, P], I),
+        "pcm_cloud_assemble": ([P, P, I64, I64, D, P, P, ctypes.POINTER(I64), P, P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -16,6 +16,7 @@
 
 #include "pcm_kernels.hpp"
 #include "pcm_kpp.hpp"
+#include "pcm_cloud.hpp"
 #include "pcm_kmeans.h"
 
 using namespace pcm;
@@ -952,5 +953,158 @@ int pcm_debug_timing(unsigned long long *out, int nblocks) {
     return 0;
 }
 #endif
+
+namespace {
+// Symmetric 3x3 eigen-solve (cyclic Jacobi, float64): eigenvector of the smallest eigenvalue.
+void smallest_eigvec3(const double cov[6], double out[3]) {
+    double a[3][3] = {{cov[0], cov[1], cov[2]}, {cov[1], cov[3], cov[4]}, {cov[2], cov[4], cov[5]}};
+    double v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int sweep = 0; sweep < 64; ++sweep) {
+        const double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+        const double diag = a[0][0] * a[0][0] + a[1][1] * a[1][1] + a[2][2] * a[2][2];
+        if (off <= 1e-40 * (diag > 0 ? diag : 1.0)) break;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                if (a[p][q] == 0.0) continue;
+                const double th = (a[q][q] - a[p][p]) / (2.0 * a[p][q]);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+                const double c = 1.0 / std::sqrt(t * t + 1.0), sn = t * c;
+                for (int k = 0; k < 3; ++k) {   // A := A J (columns p, q)
+                    const double akp = a[k][p], akq = a[k][q];
+                    a[k][p] = c * akp - sn * akq;
+                    a[k][q] = sn * akp + c * akq;
+                }
+                for (int k = 0; k < 3; ++k) {   // A := J^T A (rows p, q)
+                    const double apk = a[p][k], aqk = a[q][k];
+                    a[p][k] = c * apk - sn * aqk;
+                    a[q][k] = sn * apk + c * aqk;
+                }
+                for (int k = 0; k < 3; ++k) {   // V := V J
+                    const double vkp = v[k][p], vkq = v[k][q];
+                    v[k][p] = c * vkp - sn * vkq;
+                    v[k][q] = sn * vkp + c * vkq;
+                }
+            }
+    }
+    int m = 0;
+    for (int k = 1; k < 3; ++k)
+        if (a[k][k] < a[m][m]) m = k;
+    double nrm = std::sqrt(v[0][m] * v[0][m] + v[1][m] * v[1][m] + v[2][m] * v[2][m]);
+    for (int k = 0; k < 3; ++k) out[k] = v[k][m] / nrm;
+}
+
+// numpy.percentile(..., method='linear') on an ascending array (numpy's _lerp form).
+double percentile_linear(const double *sorted_host_lo_hi, long long n, double q, long long lo) {
+    const double vi = q / 100.0 * (double)(n - 1);
+    const double g = vi - (double)lo;
+    const double a = sorted_host_lo_hi[0], b = sorted_host_lo_hi[1];
+    const double d = b - a;
+    return g >= 0.5 ? b - d * (1.0 - g) : a + d * g;
+}
+}  // namespace
+
+// Per-pair cloud assembly (members/rafael/disparity/plugin.py:147-192).
+int pcm_cloud_assemble(const double *disparity, const uint8_t *validity, int64_t H, int64_t W, double limit,
+                       double *points, double *hnorm, int64_t *m_out, double *normal_out, void *stream) {
+    if (!disparity || !points || !hnorm || !m_out || H < 1 || W < 1) return fail(PCM_E_ARG, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    const long long n = (long long)H * W;
+    uint32_t *flags = nullptr, *pos = nullptr;
+    double *height = nullptr, *P = nullptr, *part = nullptr, *zrel = nullptr, *zsort = nullptr;
+    void *tmp = nullptr;
+    int rc = 0;
+    const int nb = blocks_for(n, CLOUD_TPB);
+    const int sb = 1024;   // reduction blocks
+    *m_out = 0;
+    do {
+        hipError_t err;
+        if ((err = hipMalloc(&flags, n * 4)) || (err = hipMalloc(&pos, n * 4)) || (err = hipMalloc(&height, n * 8)) ||
+            (err = hipMalloc(&P, n * 24)) || (err = hipMalloc(&part, (size_t)sb * 6 * 8)) ||
+            (err = hipMalloc(&zrel, n * 8)) || (err = hipMalloc(&zsort, n * 8))) {
+            rc = fail(PCM_E_NOMEM, "cloud workspace");
+            break;
+        }
+        k_cloud_flags<<<nb, CLOUD_TPB, 0, s>>>(disparity, validity, n, limit, flags, height);
+        if ((err = hipGetLastError())) { rc = fail(PCM_E_HIP, "k_cloud_flags"); break; }
+        size_t tb = 0, tb2 = 0;
+        if ((err = rocprim::exclusive_scan(nullptr, tb, flags, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s)) ||
+            (err = rocprim::radix_sort_keys(nullptr, tb2, zrel, zsort, (size_t)n, 0, 64, s)) ||
+            (err = hipMalloc(&tmp, std::max(tb, tb2)))) {
+            rc = fail(PCM_E_HIP, "cloud scan/sort setup");
+            break;
+        }
+        if ((err = rocprim::exclusive_scan(tmp, tb, flags, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s))) {
+            rc = fail(PCM_E_HIP, "cloud scan");
+            break;
+        }
+        uint32_t last_pos = 0, last_flag = 0;
+        if ((err = hipMemcpyAsync(&last_pos, pos + n - 1, 4, hipMemcpyDeviceToHost, s)) ||
+            (err = hipMemcpyAsync(&last_flag, flags + n - 1, 4, hipMemcpyDeviceToHost, s)) ||
+            (err = hipStreamSynchronize(s))) {
+            rc = fail(PCM_E_HIP, "cloud count");
+            break;
+        }
+        const long long m = (long long)last_pos + last_flag;
+        *m_out = m;
+        if (m == 0) break;
+        k_cloud_compact<<<nb, CLOUD_TPB, 0, s>>>(flags, pos, height, n, W, P);
+        const int rb = (int)std::min<long long>(sb, (m + CLOUD_TPB - 1) / CLOUD_TPB);
+        double hp[sb * 6];
+        k_cloud_sums<0><<<rb, CLOUD_TPB, 0, s>>>(P, m, 0, 0, 0, part);
+        if ((err = hipMemcpyAsync(hp, part, (size_t)rb * 3 * 8, hipMemcpyDeviceToHost, s)) ||
+            (err = hipStreamSynchronize(s))) {
+            rc = fail(PCM_E_HIP, "cloud mean");
+            break;
+        }
+        double c[3] = {0, 0, 0};
+        for (int b = 0; b < rb; ++b)
+            for (int a = 0; a < 3; ++a) c[a] += hp[b * 3 + a];
+        for (int a = 0; a < 3; ++a) c[a] /= (double)m;
+        k_cloud_sums<1><<<rb, CLOUD_TPB, 0, s>>>(P, m, c[0], c[1], c[2], part);
+        if ((err = hipMemcpyAsync(hp, part, (size_t)rb * 6 * 8, hipMemcpyDeviceToHost, s)) ||
+            (err = hipStreamSynchronize(s))) {
+            rc = fail(PCM_E_HIP, "cloud covariance");
+            break;
+        }
+        double cov[6] = {0, 0, 0, 0, 0, 0};
+        for (int b = 0; b < rb; ++b)
+            for (int a = 0; a < 6; ++a) cov[a] += hp[b * 6 + a];
+        double nv[3];
+        smallest_eigvec3(cov, nv);
+        if (nv[2] < 0) for (int a = 0; a < 3; ++a) nv[a] = -nv[a];   // plugin.py:167-168
+        if (normal_out) for (int a = 0; a < 3; ++a) normal_out[a] = nv[a];
+        const int mb = blocks_for(m, CLOUD_TPB);
+        k_cloud_project<<<mb, CLOUD_TPB, 0, s>>>(P, m, c[0], c[1], c[2], nv[0], nv[1], nv[2], zrel);
+        size_t tbs = tb2;
+        if ((err = rocprim::radix_sort_keys(tmp, tbs, zrel, zsort, (size_t)m, 0, 64, s))) {
+            rc = fail(PCM_E_HIP, "cloud sort");
+            break;
+        }
+        double q[2] = {2.0, 98.0}, hq[2];
+        for (int t = 0; t < 2; ++t) {
+            const double vi = q[t] / 100.0 * (double)(m - 1);
+            long long lo = (long long)std::floor(vi);
+            const long long hi = std::min(lo + 1, m - 1);
+            double ab[2];
+            if ((err = hipMemcpyAsync(&ab[0], zsort + lo, 8, hipMemcpyDeviceToHost, s)) ||
+                (err = hipMemcpyAsync(&ab[1], zsort + hi, 8, hipMemcpyDeviceToHost, s)) ||
+                (err = hipStreamSynchronize(s))) {
+                rc = fail(PCM_E_HIP, "cloud percentile");
+                break;
+            }
+            hq[t] = percentile_linear(ab, m, q[t], lo);
+        }
+        if (rc) break;
+        k_cloud_output<<<mb, CLOUD_TPB, 0, s>>>(P, zrel, m, hq[0], hq[1], points, hnorm);
+        if ((err = hipGetLastError()) || (err = hipStreamSynchronize(s))) {
+            rc = fail(PCM_E_HIP, std::string("cloud output: ") + hipGetErrorString(err));
+            break;
+        }
+    } while (0);
+    void *ps[] = {flags, pos, height, P, part, zrel, zsort, tmp};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    return rc;
+}
 
 }  // extern "C"

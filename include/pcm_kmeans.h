@@ -170,6 +170,17 @@ int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int 
 int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, int64_t first_index,
                  const uint64_t *umant, int scale, int64_t *indices, void *stream);
 
+/* Per-pair point-cloud assembly, replacing the float64 NumPy block of
+ * members/rafael/disparity/plugin.py:147-192 (height = -disparity/16, validity
+ * mask, np.where row-major compaction, SVD plane fit oriented to +z, relative
+ * height, 2/98 percentiles, points (z - h_min, y, x) + 'height' property).
+ * disparity: device float64[H*W]; validity: device uint8[H*W] or NULL;
+ * limit = MAX_DISP/2.  points: device float64[3*H*W] capacity, hnorm:
+ * device float64[H*W] capacity; *m_out = number of points; normal_out (host
+ * double[3], nullable) = the fitted plane normal.  Synchronises the stream. */
+int pcm_cloud_assemble(const double *disparity, const uint8_t *validity, int64_t H, int64_t W, double limit,
+                       double *points, double *hnorm, int64_t *m_out, double *normal_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
