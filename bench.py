@@ -64,6 +64,32 @@ def cpu_baseline(k: int, d: int, budget_s: float = 12.0) -> dict:
                       f"(-O3 -ffp-contract=off, OpenMP {threads} threads, {cpu_model})"}
 
 
+def cloud_bench(H: int = 4000, W: int = 4000) -> dict:
+    """Per-pair cloud assembly (plugin.py:147-192) of a synthetic HxW disparity:
+    GPU (pcm_amd.assemble_cloud, host arrays in and out, like the plugin) vs the
+    NumPy restatement (oracle/cloud_ref.py, the reference's own code path)."""
+    import torch
+
+    import pcm_amd
+    from oracle import cloud_ref
+
+    rng = np.random.default_rng(0)
+    yy, xx = np.mgrid[0:H, 0:W]
+    disp = -16.0 * (8 * np.sin(xx / 230.0) + 5 * np.cos(yy / 170.0) + rng.normal(0, 0.3, (H, W)))
+    valid = rng.random((H, W)) > 0.1
+    pcm_amd.assemble_cloud(disp[:64, :64], valid[:64, :64])      # warm-up (library, kernels)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pts, _, _ = pcm_amd.assemble_cloud(disp, valid)
+    gpu_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    ref, _, _ = cloud_ref.assemble(disp, valid)
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    assert pts.shape == ref.shape and np.array_equal(pts[:, 1:], ref[:, 1:])
+    return {"pixels": H * W, "points": int(pts.shape[0]), "gpu_ms": gpu_ms, "cpu_numpy_ms": cpu_ms,
+            "note": "host float64 disparity in, host (M,3) points out (PCIe included)"}
+
+
 def pmc_traffic(n, k, d, world):
     """HBM bytes per k_lloyd launch from a rocprofv3 --pmc summary of this same
     workload (tools/evidence.sh; FETCH_SIZE x2 for gfx950's halved wide-read
@@ -89,6 +115,8 @@ def main():
     ap.add_argument("--d", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fit", action="store_true", help="also time one whole 20-iteration fit")
+    ap.add_argument("--cloud", action="store_true",
+                    help="also time the per-pair cloud assembly (4000x4000 disparity) on GPU and CPU")
     args = ap.parse_args()
 
     import torch
@@ -213,6 +241,8 @@ def main():
         }
         if fit_ms is not None:
             out["fit_20_iters_ms"] = fit_ms
+        if args.cloud:
+            out["cloud_assembly"] = cloud_bench()
         if kpp_ms is not None:
             out["kmeanspp_ms"] = kpp_ms   # GPU k-means++ seeding of the same cloud (K centres), host prep included
         if not args.no_cpu:

@@ -14,5 +14,5 @@ for P in FETCH_SIZE WRITE_SIZE; do
 done
 python tools/pmc_summary.py k_lloyd $T/pmc_FETCH_SIZE $T/pmc_WRITE_SIZE > $T/pmc_k_lloyd.json && cat $T/pmc_k_lloyd.json
 bash tools/prof.sh $T/prof --steps 20 --warmup 3 | tail -8 || exit 1
-PCM_PMC_JSON=$T/pmc_k_lloyd.json timeout -k 10 400 python bench.py --fit > $T/bench.txt 2>&1 || { tail -20 $T/bench.txt; exit 1; }
+PCM_PMC_JSON=$T/pmc_k_lloyd.json timeout -k 10 400 python bench.py --fit --cloud > $T/bench.txt 2>&1 || { tail -20 $T/bench.txt; exit 1; }
 tail -1 $T/bench.txt
