@@ -115,6 +115,11 @@ def main():
     ap.add_argument("--d", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fit", action="store_true", help="also time one whole 20-iteration fit")
+    ap.add_argument("--split", action="store_true",
+                    help="one GPU through the multi-GPU call sequence (nccl group of 1; calibration)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the multi-GPU iteration sequence (incl. the RCCL all-reduce) in a HIP graph")
+    ap.add_argument("--no-events", action="store_true", help="calibration: no per-kernel HIP events")
     ap.add_argument("--cloud", action="store_true",
                     help="also time the per-pair cloud assembly (4000x4000 disparity) on GPU and CPU")
     args = ap.parse_args()
@@ -128,6 +133,10 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif args.split:
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29533", world_size=1, rank=0,
+                                device_id=torch.device("cuda", local))
+    multi = world > 1 or args.split
 
     import pcm_amd
     from pcm_amd import lloyd
@@ -140,7 +149,7 @@ def main():
     init_rows = np.sort(np.random.default_rng(1).choice(N, K, replace=False))
     C0 = synth_rows(init_rows, D, seed=0)
     total_iters = args.warmup + args.steps
-    max_iter = total_iters + 8
+    max_iter = total_iters + 16
     group = None
 
     eng = Engine(D, K, torch.float32, max_iter=max_iter)
@@ -154,7 +163,7 @@ def main():
     eng.begin(C0, 0.0, max_iter)
 
     def iterate(n):
-        if world == 1:
+        if not multi:
             eng.iterate(n)
         else:
             for _ in range(n):
@@ -162,24 +171,50 @@ def main():
                 dist.all_reduce(eng.stats)
                 eng.iter_global()
 
+    graph = None
+    if multi and args.graph:
+        # the timed steps as one captured graph (k_lloyd, k_fold, RCCL all-reduce, k_step per step)
+        graph = torch.cuda.CUDAGraph()
+
     iterate(args.warmup)
     torch.cuda.synchronize()
     st = eng.status()
     if st["halt"] or st["done"]:
         raise SystemExit(f"fit stopped during warm-up: {st}")
-    eng.timing(True)
+    if graph is not None:
+        with torch.cuda.graph(graph):
+            iterate(args.steps)
+        torch.cuda.synchronize()
+        # capture recorded the launches without running them
+        if eng.status()["iter"] != args.warmup:
+            raise SystemExit("graph capture executed iterations")
+    elif not args.no_events and world == 1:
+        # per-kernel HIP events inside the timed region (they cost ~5 us/iter here;
+        # at N>1 the shards are small and the events would cost ~15 %, so there
+        # the per-kernel times come from a separate pass after the timed region)
+        eng.timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    iterate(args.steps)
+    if graph is not None:
+        graph.replay()
+    else:
+        iterate(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    tm = eng.timing_read()
+    if graph is None and not args.no_events and world == 1:
+        tm = eng.timing_read()
+    elif not args.no_events and world > 1:
+        eng.timing(True)
+        iterate(4)   # untimed: per-kernel durations for the roofline line
+        tm = eng.timing_read()
+    else:
+        tm = {"assign_ms": 0.0, "tail_ms": 0.0}
     st = eng.status()
-    if st["iter"] != total_iters or st["halt"]:
+    if st["iter"] < total_iters or st["halt"]:
         raise SystemExit(f"timed iterations did not all run: {st}")
     cand = eng.candidate_stats()
     info = eng.layout_info()
@@ -248,7 +283,7 @@ def main():
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(K, D)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
