@@ -142,14 +142,16 @@ void free_layout(pcm_engine *e) {
     e->fit_ready = false;
 }
 
-// Choose the pruning grid: about min(32 K, n / 1024) roughly cubic cells over
+// Choose the pruning grid: about min(32 K, n / 2800) roughly cubic cells over
 // the bounding box (degenerate axes get one cell).
 void choose_grid(pcm_engine *e) {
     Grid &g = e->g;
     g = Grid{};
     g.d = e->d;
     g.F = 4;   // fixed: k_cand assumes 4 fine cells per coarse cell per axis
-    double target = std::min(32.0 * e->k, (double)e->n / 1024.0);
+    // ~2.8k points per cell: fewer, fuller tiles (a tile round is 1024 points)
+    // outweigh the slightly longer candidate lists (swept on 12.5M / 100M clouds)
+    double target = std::min(32.0 * e->k, (double)e->n / 2800.0);
     if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     target = std::max(1.0, std::min(target, (double)(1 << 18)));
     double vol = 1.0;
@@ -483,11 +485,21 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
     return launch_candidates(e, s, 0);
 }
 
+// Candidate blocks per coarse cell: enough blocks to fill the chip on small
+// (sharded) clouds; D = 4 coarse cells hold 256 fine cells.
+static int cand_bpc(const pcm_engine *e) {
+    if (const char *ov = std::getenv("PCM_CAND_BPC_RT")) return std::max(1, std::atoi(ov));   // tuning sweeps only
+    if (e->d >= 4) return 16;
+    long long b = ((long long)e->num_cu + e->g.ncoarse - 1) / std::max(1LL, e->g.ncoarse);
+    return (int)std::max(1LL, std::min(8LL, b));
+}
+
 static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_cand<D><<<(int)(e->g.ncoarse * cand_bpc<D>()), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
-                                                                 e->ctrl, gate);
+        const int bpc = cand_bpc(e);
+        k_cand<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
+                                                                 e->ctrl, gate, bpc);
         LAUNCHCHK();
         return 0;
     });
@@ -613,9 +625,10 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
     int rc = dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
         if (e->k <= KSTEP_MAX && !resume_path) {
-            k_step<D><<<(int)(e->g.ncoarse * cand_bpc<D>() + 1), CAND_TPB, (size_t)e->k * sizeof(float4), s>>>(
+            const int bpc = cand_bpc(e);
+            k_step<D><<<(int)(e->g.ncoarse * bpc + 1), CAND_TPB, (size_t)e->k * sizeof(float4), s>>>(
                 e->g, from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C,
-                e->hist_changed, e->hist_shift, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab);
+                e->hist_changed, e->hist_shift, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab, bpc);
             LAUNCHCHK();
             return 0;
         }

@@ -287,12 +287,7 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
 //     centre (again an LDS atomic-min key), keep the parent candidates it does
 //     not dominate, in ascending centroid order (the scan's tie rule); the count
 //     goes to fc_cnt[cell] (FULL = more than CAPF, or pruning disabled).
-#ifndef PCM_CAND_BPC
-#define PCM_CAND_BPC 1
-#endif
-constexpr int CAND_BPC = PCM_CAND_BPC;   // blocks per coarse cell (D <= 3)
 // D = 4: a coarse cell has 4^4 = 256 fine cells and a longer coarse list
-template <int D> constexpr int cand_bpc() { return D >= 4 ? 16 : CAND_BPC; }
 template <int D> constexpr int cand_capc() { return D >= 4 ? 1024 : CAPC; }
 #ifndef PCM_CAND_TPB
 #define PCM_CAND_TPB 256
@@ -324,8 +319,8 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // C: the K centres, in global memory (k_cand) or in LDS (k_step).
 template <int D>
 __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K, uint32_t *__restrict__ fc_cnt,
-                                          float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab) {
-    constexpr int BPC = cand_bpc<D>(), CAP = cand_capc<D>();
+                                          float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab, int BPC) {
+    constexpr int CAP = cand_capc<D>();
     const long long I = blockIdx.x / BPC;
     const int bsub = blockIdx.x % BPC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -508,9 +503,10 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
 template <int D>
 __global__ __launch_bounds__(CAND_TPB) void k_cand(Grid g, const float4 *__restrict__ C, int K,
                                               uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                              int32_t *__restrict__ fc_lab, const Ctrl *__restrict__ ctrl, int gate) {
+                                              int32_t *__restrict__ fc_lab, const Ctrl *__restrict__ ctrl, int gate,
+                                              int bpc) {
     if (gate && gated(ctrl)) return;
-    cand_body<D>(g, C, K, fc_cnt, fc_rec, fc_lab);
+    cand_body<D>(g, C, K, fc_cnt, fc_rec, fc_lab, bpc);
 }
 
 // ------------------------------------------------------------------ assign
@@ -1169,7 +1165,7 @@ __global__ __launch_bounds__(CAND_TPB) void k_step(Grid g, const unsigned long l
                                               unsigned long long *__restrict__ hist_changed,
                                               double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl,
                                               uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                              int32_t *__restrict__ fc_lab) {
+                                              int32_t *__restrict__ fc_lab, int bpc) {
     if (gated(ctrl)) return;
     DBG_T(0);
     extern __shared__ __attribute__((aligned(16))) float4 cn[];   // [K]
@@ -1262,7 +1258,7 @@ __global__ __launch_bounds__(CAND_TPB) void k_step(Grid g, const unsigned long l
         }
     }
     DBG_T(3);
-    if (!b0) cand_body<D>(g, cn, K, fc_cnt, fc_rec, fc_lab);
+    if (!b0) cand_body<D>(g, cn, K, fc_cnt, fc_rec, fc_lab, bpc);
     // Every block has read ctrl->iter (parity) before any block can observe the
     // final count, so only the last block advances the iteration and flags.
     __syncthreads();
