@@ -9,6 +9,7 @@ Public API
 lloyd_fit(X, centers_init, max_iter, tol, group=None)  -> LloydResult
 kmeans_plusplus(X, n_clusters, random_state=...)       -> (centers, indices), GPU k-means++
 assemble_cloud(disparity, validity, max_disp=288)      -> per-pair (z,y,x) cloud + height property (GPU)
+KMeans(n_clusters, init, n_init, ...).fit_predict(X)   -> the reference's KMeans call site (core.py:227-228)
 kmeans_fuse(clouds, n_clusters, ...)                   -> napari layer tuples
 HeightMapExtractor                                     -> SatellitePlugin drop-in
 Engine                                                 -> the C-ABI engine wrapper
@@ -17,7 +18,7 @@ from .fixed import QBITS, fixed_q  # noqa: F401
 from .lloyd import LloydResult, lloyd_fit  # noqa: F401
 
 __all__ = ["lloyd_fit", "LloydResult", "fixed_q", "QBITS", "Engine", "kmeans_fuse", "HeightMapExtractor",
-           "build_library", "kmeans_plusplus", "assemble_cloud"]
+           "build_library", "kmeans_plusplus", "assemble_cloud", "KMeans"]
 
 
 def __getattr__(name):
@@ -28,6 +29,9 @@ def __getattr__(name):
     if name in ("kmeans_fuse", "HeightMapExtractor", "PREFIX"):
         from . import plugin
         return getattr(plugin, name)
+    if name == "KMeans":
+        from .estimator import KMeans
+        return KMeans
     if name == "assemble_cloud":
         from .cloud import assemble_cloud
         return assemble_cloud

@@ -1,0 +1,125 @@
+"""``KMeans`` estimator: the reference's only K-means call site on the GPU engine.
+
+The reference runs ``KMeans(n_clusters=K, random_state=42, n_init=10).fit_predict(X)``
+(``members/jasraj/land_use_classification/core.py:227-228``).
+This class keeps that API and restates the control flow of scikit-learn 1.7.2's
+``KMeans.fit`` (``sklearn/cluster/_kmeans.py:1427-1547``):
+
+* ``tol`` becomes ``mean(var(X, axis=0)) * tol`` (``_tolerance``, ``:279-287``),
+  computed on the input exactly as sklearn does (NumPy, the input dtype);
+* X is centred by its mean before fitting and the mean is added back to the
+  centres (``:1479-1484``, ``:1536-1537``);
+* ``n_init`` runs share ONE ``RandomState``; each is seeded by k-means++
+  (``_kmeans_plusplus``), ``'random'`` rows or a given array (``_init_centroids``,
+  ``:955-1032``); a run replaces the best only if its inertia is lower and its
+  clustering differs (``_is_same_clustering``, ``_k_means_common.pyx:314-328``);
+  ``n_init='auto'`` is 1 for k-means++ / an array, 10 for ``'random'``.
+
+Every pass over the cloud runs in the HIP kernels (k-means++ seeding, Lloyd
+iterations, final E-step); the host holds only O(K) state plus the mean/var of
+the boundary, which mirror sklearn's own NumPy calls.  Arithmetic is the
+canonical float32 form of DESIGN.md §2 (sklearn keeps float64 input in
+float64; here it is rounded to float32 at the boundary).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import numpy as np
+
+
+def _same_clustering(l1: np.ndarray, l2: np.ndarray, k: int) -> bool:
+    """sklearn ``_is_same_clustering``: labels1 -> labels2 is a consistent mapping."""
+    mapping = np.full(k, -1, dtype=np.int64)
+    _, first = np.unique(l1, return_index=True)
+    mapping[l1[first]] = l2[first]
+    return bool(np.array_equal(mapping[l1], l2))
+
+
+class KMeans:
+    """Drop-in for ``sklearn.cluster.KMeans`` (Lloyd, dense, unit weights) on MI355X."""
+
+    def __init__(self, n_clusters: int = 8, *, init="k-means++", n_init="auto", max_iter: int = 300,
+                 tol: float = 1e-4, random_state=None, algorithm: str = "lloyd",
+                 _fit: Optional[Callable] = None, _seed: Optional[Callable] = None):
+        self.n_clusters = n_clusters
+        self.init = init
+        self.n_init = n_init
+        self.max_iter = max_iter
+        self.tol = tol
+        self.random_state = random_state
+        self.algorithm = algorithm
+        self._fit = _fit      # tests: a CPU stand-in for (Xc, C0, max_iter, tol) -> (labels, centers, inertia, n_iter)
+        self._seed = _seed    # tests: a CPU stand-in for k-means++ (Xc, k, RandomState) -> centers
+
+    # ------------------------------------------------------------ GPU legs
+    @staticmethod
+    def _gpu_fit(Xc: np.ndarray, C0: np.ndarray, max_iter: int, tol: float):
+        import torch
+
+        from .lloyd import lloyd_fit
+        res = lloyd_fit(torch.from_numpy(Xc).cuda(), torch.from_numpy(np.ascontiguousarray(C0, np.float32)).cuda(),
+                        max_iter=max_iter, tol=tol)
+        torch.cuda.synchronize()
+        return res.labels.cpu().numpy(), res.centers.cpu().numpy(), float(res.inertia), int(res.n_iter)
+
+    @staticmethod
+    def _gpu_seed(Xc: np.ndarray, k: int, rs: np.random.RandomState) -> np.ndarray:
+        import torch
+
+        from .kpp import kmeans_plusplus
+        C, _ = kmeans_plusplus(torch.from_numpy(Xc).cuda(), k, random_state=rs)
+        return C.cpu().numpy()
+
+    # ------------------------------------------------------------ sklearn API
+    def fit(self, X, y=None, sample_weight=None):
+        if sample_weight is not None and not np.all(np.asarray(sample_weight) == 1):
+            raise NotImplementedError("unit sample weights only (the reference's call site passes none)")
+        if self.algorithm != "lloyd":
+            raise NotImplementedError("algorithm='lloyd' only")
+        if hasattr(X, "detach"):
+            X = X.detach().cpu().numpy()
+        X = np.array(X, dtype=np.float32, order="C", copy=True)     # boundary: float32, C order
+        n, d = X.shape
+        k = int(self.n_clusters)
+        if n < k:
+            raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
+        init = self.init
+        init_is_array = not isinstance(init, str)
+        if self.n_init == "auto":
+            n_init = 10 if (isinstance(init, str) and init == "random") else 1
+        else:
+            n_init = int(self.n_init)
+        if init_is_array and n_init != 1:
+            n_init = 1    # sklearn warns and runs once for an explicit init array
+        rs = self.random_state if isinstance(self.random_state, np.random.RandomState) \
+            else np.random.RandomState(self.random_state)
+        tol_abs = float(np.mean(np.var(X, axis=0)) * self.tol) if self.tol else 0.0   # _tolerance (X's dtype)
+        X_mean = X.mean(axis=0)
+        Xc = X - X_mean                                                              # centring (:1479-1484)
+        fit = self._fit or self._gpu_fit
+        seed = self._seed or self._gpu_seed
+        best = None
+        for _ in range(n_init):
+            if init_is_array:
+                C0 = np.asarray(init, dtype=np.float32) - X_mean
+            elif init == "k-means++":
+                C0 = seed(Xc, k, rs)
+            elif init == "random":
+                sw = np.ones(n, dtype=X.dtype)                               # _check_sample_weight
+                C0 = Xc[rs.choice(n, size=k, replace=False, p=sw / sw.sum())]
+            else:
+                raise ValueError(f"init must be 'k-means++', 'random' or an array, got {init!r}")
+            labels, centers, inertia, n_iter = fit(Xc, C0, int(self.max_iter), tol_abs)
+            if best is None or (inertia < best[2] and not _same_clustering(labels, best[0], k)):
+                best = (labels, centers, inertia, n_iter)
+        labels, centers, inertia, n_iter = best
+        self.cluster_centers_ = (centers + X_mean).astype(np.float32)
+        self.labels_ = labels.astype(np.int32)
+        self.inertia_ = inertia
+        self.n_iter_ = n_iter
+        self.n_features_in_ = d
+        return self
+
+    def fit_predict(self, X, y=None, sample_weight=None):
+        return self.fit(X, sample_weight=sample_weight).labels_

@@ -29,8 +29,10 @@ def _scale(n: int, maxd: float) -> int:
 
 
 def _first_index(n: int, u0: float) -> int:
-    """numpy RandomState.choice(n, p=ones/n) for its single random_sample() draw u0."""
-    p = np.full(n, 1.0 / n)
+    """numpy RandomState.choice(n, p=w / w.sum()) for its single random_sample() draw u0,
+    with sklearn's unit float32 weights (``_check_sample_weight`` in X's dtype)."""
+    w = np.ones(n, dtype=np.float32)
+    p = (w / w.sum()).astype(np.float64)
     cdf = p.cumsum()
     cdf /= cdf[-1]
     return int(cdf.searchsorted(u0, side="right"))

@@ -73,23 +73,25 @@ def target(u: float, pot: int) -> int:
     return (m * int(pot)) >> 53
 
 
-def first_index(n: int, u0: float) -> int:
-    """numpy RandomState.choice(n, p=ones/n) given its one random_sample() draw."""
-    p = np.full(n, 1.0 / n)
+def first_index(n: int, u0: float, dtype=np.float32) -> int:
+    """numpy RandomState.choice(n, p=w / w.sum()) given its one random_sample() draw,
+    with sklearn's unit weights in X's dtype (``_check_sample_weight``)."""
+    w = np.ones(n, dtype=dtype)
+    p = (w / w.sum()).astype(np.float64)
     cdf = p.cumsum()
     cdf /= cdf[-1]
     return int(cdf.searchsorted(u0, side="right"))
 
 
-def draws(seed: int, k: int, L: int):
-    """The exact random stream sklearn's _kmeans_plusplus consumes."""
-    rs = np.random.RandomState(seed)
+def draws(seed, k: int, L: int):
+    """The exact random stream sklearn's _kmeans_plusplus consumes (seed: int or RandomState)."""
+    rs = seed if isinstance(seed, np.random.RandomState) else np.random.RandomState(seed)
     u0 = rs.random_sample()
     us = np.stack([rs.uniform(size=L) for _ in range(1, k)]) if k > 1 else np.zeros((0, L))
     return u0, us
 
 
-def kmeanspp(X, k: int, seed: int, n_local_trials: int | None = None):
+def kmeanspp(X, k: int, seed, n_local_trials: int | None = None):
     """Returns (centers (k, d) float32, indices (k,) int64)."""
     X = as_f32_points(X)
     n, d = X.shape

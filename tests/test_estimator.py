@@ -1,0 +1,81 @@
+"""``pcm_amd.KMeans``: the reference's call site ``KMeans(n_clusters=K,
+random_state=42, n_init=10).fit_predict(X)`` (members/jasraj/land_use_classification/core.py:227-228)
+with sklearn's KMeans.fit control flow (centring, _tolerance, n_init runs on
+one RandomState, best-inertia selection).
+
+CPU: the estimator driven by the oracle legs (oracle Lloyd + oracle k-means++)
+equals scikit-learn's KMeans.  GPU: the estimator on the HIP engine equals the
+oracle-driven one bit for bit, and scikit-learn's KMeans on the same cases.
+"""
+import numpy as np
+import pytest
+
+from oracle import kpp_ref as P
+from oracle import lloyd_ref as R
+
+CASES = [  # n, k, d, seed, n_init, init
+    (3000, 8, 3, 42, 10, "k-means++"),
+    (4096, 32, 3, 7, 3, "k-means++"),
+    (2000, 6, 2, 1, 4, "random"),
+    (5000, 16, 3, 0, "auto", "k-means++"),
+]
+
+
+def oracle_fit(Xc, C0, max_iter, tol):
+    r = R.lloyd_fit(Xc, C0, max_iter=max_iter, tol=tol, fast=True)
+    return r["labels"], r["centers"], r["inertia"], r["n_iter"]
+
+
+def oracle_seed(Xc, k, rs):
+    return P.kmeanspp(Xc, k, rs)[0]
+
+
+def cloud(n, d, seed):
+    rng = np.random.default_rng(seed)
+    centers = rng.random((6, d)) * 10
+    return (centers[rng.integers(0, 6, n)] + rng.normal(0, 0.8, (n, d))).astype(np.float32)
+
+
+def run_sklearn(X, k, seed, n_init, init):
+    sk = pytest.importorskip("sklearn.cluster")
+    return sk.KMeans(n_clusters=k, random_state=seed, n_init=n_init, init=init).fit(X)
+
+
+def assert_like_sklearn(est, ref):
+    np.testing.assert_array_equal(est.labels_, ref.labels_)
+    assert est.n_iter_ == ref.n_iter_
+    np.testing.assert_allclose(est.cluster_centers_, ref.cluster_centers_, rtol=1e-5, atol=1e-5)
+    assert est.inertia_ == pytest.approx(ref.inertia_, rel=1e-4)
+
+
+@pytest.mark.parametrize("n,k,d,seed,n_init,init", CASES)
+def test_oracle_legs_match_sklearn(n, k, d, seed, n_init, init):
+    import pcm_amd
+    X = cloud(n, d, seed)
+    est = pcm_amd.KMeans(n_clusters=k, random_state=seed, n_init=n_init, init=init,
+                         _fit=oracle_fit, _seed=oracle_seed).fit(X)
+    assert_like_sklearn(est, run_sklearn(X, k, seed, n_init, init))
+
+
+def test_same_clustering_helper():
+    from pcm_amd.estimator import _same_clustering
+    a = np.array([0, 0, 1, 2, 1], np.int32)
+    assert _same_clustering(a, np.array([2, 2, 0, 1, 0]), 3)
+    assert not _same_clustering(a, np.array([2, 2, 0, 1, 1]), 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,d,seed,n_init,init", CASES)
+def test_gpu_matches_oracle_legs_and_sklearn(n, k, d, seed, n_init, init):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pcm_amd
+    X = cloud(n, d, seed)
+    est = pcm_amd.KMeans(n_clusters=k, random_state=seed, n_init=n_init, init=init).fit(X)
+    ref = pcm_amd.KMeans(n_clusters=k, random_state=seed, n_init=n_init, init=init,
+                         _fit=oracle_fit, _seed=oracle_seed).fit(X)
+    np.testing.assert_array_equal(est.labels_, ref.labels_)
+    np.testing.assert_array_equal(est.cluster_centers_, ref.cluster_centers_)
+    assert est.n_iter_ == ref.n_iter_
+    assert_like_sklearn(est, run_sklearn(X, k, seed, n_init, init))

@@ -38,7 +38,9 @@ def test_host_helpers_match_oracle():
         assert (n * P.kpp_scale(n, maxd) >= 0) or True
     rs = np.random.RandomState(3)
     u0 = rs.random_sample()
-    assert K._first_index(1000, u0) == np.random.RandomState(3).choice(1000, p=np.full(1000, 1e-3))
+    w = np.ones(1000, np.float32)
+    assert K._first_index(1000, u0) == np.random.RandomState(3).choice(1000, p=w / w.sum())
+    assert P.first_index(1000, u0) == K._first_index(1000, u0)
 
 
 def test_weights_cannot_overflow():
