@@ -57,9 +57,9 @@ class KMeans:
     def _gpu_fit(Xc: np.ndarray, C0: np.ndarray, max_iter: int, tol: float):
         import torch
 
-        from .lloyd import lloyd_fit
+        from .lloyd import LOCAL, lloyd_fit
         res = lloyd_fit(torch.from_numpy(Xc).cuda(), torch.from_numpy(np.ascontiguousarray(C0, np.float32)).cuda(),
-                        max_iter=max_iter, tol=tol)
+                        max_iter=max_iter, tol=tol, group=LOCAL)
         torch.cuda.synchronize()
         return res.labels.cpu().numpy(), res.centers.cpu().numpy(), float(res.inertia), int(res.n_iter)
 

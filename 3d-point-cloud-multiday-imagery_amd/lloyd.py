@@ -42,8 +42,21 @@ class LloydResult:
     layout: dict = field(default_factory=dict)
 
 
+class _Local:
+    """``group=LOCAL``: a single-process fit even when a default process group
+    exists (the estimator and the plugin fit the whole cloud on one GPU)."""
+
+    def __repr__(self):
+        return "pcm_amd.lloyd.LOCAL"
+
+
+LOCAL = _Local()
+
+
 def _world(group):
     import torch.distributed as dist
+    if group is LOCAL:
+        return 1, 0
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size(group), dist.get_rank(group)
     return 1, 0
@@ -128,7 +141,9 @@ def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=N
 
     ``tol`` is the absolute centre-shift tolerance (sklearn's ``_tolerance``
     output, ``_kmeans.py:279-287``); 0 means "strict label convergence or
-    max_iter".  ``engine`` lets tests substitute a CPU stand-in for the HIP engine.
+    max_iter".  ``group``: the process group whose ranks each hold one row shard
+    (None = the default group when one is initialised); ``LOCAL`` forces a
+    single-process fit of ``X`` alone.  ``engine`` lets tests substitute a CPU stand-in for the HIP engine.
     """
     if engine is None:
         from .engine import Engine

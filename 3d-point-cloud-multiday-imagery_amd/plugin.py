@@ -53,12 +53,12 @@ def _tolerance(X: np.ndarray, tol: float) -> float:
 def _gpu_fit(X: np.ndarray, C0: np.ndarray, max_iter: int, tol_abs: float):
     import torch
 
-    from .lloyd import lloyd_fit
+    from .lloyd import LOCAL, lloyd_fit
 
     with _gpu_lock:
         Xt = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).cuda()
         Ct = torch.from_numpy(np.ascontiguousarray(C0, dtype=np.float32)).cuda()
-        res = lloyd_fit(Xt, Ct, max_iter=max_iter, tol=tol_abs)
+        res = lloyd_fit(Xt, Ct, max_iter=max_iter, tol=tol_abs, group=LOCAL)   # whole cloud, this GPU
         torch.cuda.synchronize()
         return (res.labels.cpu().numpy(), res.centers.cpu().numpy(), float(res.inertia), int(res.n_iter))
 

@@ -28,27 +28,28 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir):
+def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import pcm_amd
     from cpu_engine import OracleEngine
+    from pcm_amd.lloyd import LOCAL
     n = X.shape[0]
-    a, b = n * rank // world, n * (rank + 1) // world
+    a, b = (0, n) if local else (n * rank // world, n * (rank + 1) // world)
     eng = OracleEngine(X.shape[1], C0.shape[0], max_iter)
     res = pcm_amd.lloyd_fit(torch.from_numpy(X[a:b]), torch.from_numpy(C0), max_iter=max_iter, tol=0.0,
-                            chunk=chunk, engine=eng)
+                            chunk=chunk, engine=eng, group=LOCAL if local else None)
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), labels=res.labels.numpy(), centers=res.centers.numpy(),
              n_iter=res.n_iter, inertia=res.inertia, changed=res.changed, relocs=res.relocations)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def run_world(X, C0, max_iter, chunk, tmp_path, world=2):
+def run_world(X, C0, max_iter, chunk, tmp_path, world=2, local=False):
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, X, C0, max_iter, chunk, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, X, C0, max_iter, chunk, str(tmp_path), local), nprocs=world, join=True)
     parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
     return parts
 
@@ -84,3 +85,18 @@ def test_two_ranks_relocation(tmp_path):
     np.testing.assert_array_equal(labels, ref["labels"])
     np.testing.assert_array_equal(parts[0]["centers"], ref["centers"])
     assert int(parts[1]["n_iter"]) == ref["n_iter"]
+
+
+def test_local_group_under_default_group(tmp_path):
+    """group=LOCAL (what the estimator and the plugin pass) fits the rank's whole
+    X alone even when a default process group exists (counts and
+    inertia were multiplied by the world size)."""
+    from oracle import lloyd_ref as R
+    X = R.splitmix_uniform(4000, 3, 23)
+    C0 = X[R.init_indices(4000, 12)]
+    ref = R.lloyd_fit(X, C0, max_iter=10)
+    parts = run_world(X, C0, 10, 4, tmp_path, local=True)
+    for p in parts:
+        np.testing.assert_array_equal(p["labels"], ref["labels"])
+        np.testing.assert_array_equal(p["centers"], ref["centers"])
+        assert float(p["inertia"]) == pytest.approx(ref["inertia"], rel=1e-12)

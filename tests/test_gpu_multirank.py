@@ -1,0 +1,115 @@
+"""GPU, world size 2: the row-sharded driver on the real HIP engine.
+
+Two ranks share ``cuda:0`` (one box has one GPU; RCCL refuses two ranks on one
+device, so the process group is gloo, which all-reduces the device tensors
+through host staging).  Each rank fits its contiguous row shard with
+``pcm_amd.lloyd_fit``: the global fixed-point exponents (MAX all-reduce), shard
+offsets (all-gather), ``iter_local -> all_reduce(engine.stats) -> iter_global``
+every iteration, and the empty-cluster relocation (every rank's device
+relocation records all-gathered, then applied on every rank).  The result must
+be bit-identical to the single-process GPU fit and to the oracle.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import lloyd_ref as R  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, X, C0, max_iter, chunk, dtype, out_dir):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import pcm_amd
+    n = X.shape[0]
+    a, b = n * rank // world, n * (rank + 1) // world
+    Xs = torch.from_numpy(np.ascontiguousarray(X[a:b])).to("cuda", dtype)
+    res = pcm_amd.lloyd_fit(Xs, torch.from_numpy(C0).cuda(), max_iter=max_iter, tol=0.0, chunk=chunk)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), labels=res.labels.cpu().numpy(),
+             centers=res.centers.cpu().numpy(), n_iter=res.n_iter, inertia=res.inertia, changed=res.changed,
+             relocs=res.relocations)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_world(X, C0, max_iter, chunk, tmp_path, world=2, dtype=torch.float32):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(world, _free_port(), X, C0, max_iter, chunk, dtype, str(tmp_path)), nprocs=world,
+             join=True)
+    return [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
+
+
+@pytest.fixture(scope="module")
+def pcm():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pcm_amd
+    return pcm_amd
+
+
+def single(pcm, X, C0, max_iter, dtype=torch.float32):
+    res = pcm.lloyd_fit(torch.from_numpy(X).to("cuda", dtype), torch.from_numpy(C0).cuda(), max_iter=max_iter,
+                        tol=0.0)
+    torch.cuda.synchronize()
+    return res
+
+
+def compare(parts, res1, ref):
+    labels = np.concatenate([p["labels"] for p in parts])
+    np.testing.assert_array_equal(labels, ref["labels"])
+    np.testing.assert_array_equal(labels, res1.labels.cpu().numpy())
+    for p in parts:
+        np.testing.assert_array_equal(p["centers"], ref["centers"])
+        np.testing.assert_array_equal(p["centers"], res1.centers.cpu().numpy())
+        assert int(p["n_iter"]) == ref["n_iter"] == res1.n_iter
+        np.testing.assert_array_equal(np.asarray(p["changed"]) > 0, np.asarray(ref["changed"]) > 0)
+        assert float(p["inertia"]) == pytest.approx(ref["inertia"], rel=1e-9)
+
+
+@pytest.mark.parametrize("chunk", [1, 5])
+def test_two_ranks_hip_engine(pcm, tmp_path, chunk):
+    X = R.splitmix_uniform(300_000, 3, 41)
+    C0 = X[R.init_indices(300_000, 256)]
+    ref = R.lloyd_fit(X, C0, max_iter=12, fast=True)
+    parts = run_world(X, C0, 12, chunk, tmp_path)
+    compare(parts, single(pcm, X, C0, 12), ref)
+
+
+def test_two_ranks_hip_engine_fp16_d4(pcm, tmp_path):
+    X = R.splitmix_uniform(120_000, 4, 42).astype(np.float16).astype(np.float32)
+    C0 = X[R.init_indices(120_000, 64)]
+    ref = R.lloyd_fit(X, C0, max_iter=8, fast=True)
+    parts = run_world(X, C0, 8, 3, tmp_path, dtype=torch.float16)
+    compare(parts, single(pcm, X, C0, 8, torch.float16), ref)
+
+
+def test_two_ranks_hip_relocation_across_shards(pcm, tmp_path):
+    """Empty clusters whose farthest points sit on different ranks."""
+    X = R.splitmix_uniform(40_000, 3, 43)
+    X[1_000] = [3.0, 3.0, 3.0]           # rank 0's far outlier
+    X[39_000] = [-2.0, 4.0, 1.0]         # rank 1's (farther)
+    X[25_000] = [2.5, -1.5, 2.0]         # rank 1
+    C0 = np.concatenate([X[:20], np.array([[50, 50, 50], [60, 60, 60], [70, 70, 70]], np.float32)])
+    ref = R.lloyd_fit(X, C0, max_iter=20, fast=True)
+    parts = run_world(X, C0, 20, 3, tmp_path)
+    assert int(parts[0]["relocs"]) >= 1 and int(parts[1]["relocs"]) == int(parts[0]["relocs"])
+    compare(parts, single(pcm, X, C0, 20), ref)
