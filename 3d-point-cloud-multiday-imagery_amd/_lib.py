@@ -27,7 +27,9 @@ EXPORTS = [
     "pcm_bind_stats", "pcm_reloc_candidates", "pcm_reloc_apply", "pcm_final", "pcm_labels", "pcm_get_centers",
     "pcm_history", "pcm_read_status", "pcm_layout_info", "pcm_candidate_stats", "pcm_synth_uniform",
     "pcm_assign_bruteforce", "pcm_timing", "pcm_timing_read", "pcm_synth_rows", "pcm_kmeanspp", "pcm_cloud_assemble",
+    "pcm_inertia_value",
 ]
+ABI_VERSION = 2
 
 _lock = threading.Lock()
 _lib = None
@@ -40,7 +42,8 @@ class PcmError(RuntimeError):
 class PcmStatus(ctypes.Structure):
     _fields_ = [("halt", ctypes.c_uint32), ("done", ctypes.c_uint32), ("iter", ctypes.c_uint32),
                 ("n_empty", ctypes.c_uint32), ("inertia", ctypes.c_double), ("last_changed", ctypes.c_uint64),
-                ("last_shift", ctypes.c_double)]
+                ("last_shift", ctypes.c_double), ("inertia_limbs", ctypes.c_uint64 * 3),
+                ("inertia_scale", ctypes.c_int32), ("inertia_overflow", ctypes.c_uint32)]
 
 
 def needs_build() -> bool:
@@ -93,6 +96,7 @@ def _declare(lib):
         "pcm_synth_rows": ([P, P, I64, I, ctypes.c_uint64, P], I),
         "pcm_kmeanspp": ([P, I64, I, I, I, I64, P, I, P, P], I),
         "pcm_cloud_assemble": ([P, P, I64, I64, D, P, P, ctypes.POINTER(I64), P, P], I),
+        "pcm_inertia_value": ([P, I, ctypes.c_uint32], D),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -47,8 +47,9 @@ struct pcm_engine {
     bool have_bbox = false, layout_ready = false, fit_ready = false;
     Grid g{};
     QExp qe{};
-    long long ntiles = 0;
-    // device buffers
+    long long ntiles = 0;            // host copy: -1 = not read back yet (pcm_layout_info reads it)
+    long long ntiles_cap = 0;        // upper bound on the tiles of the current layout (grid sizing)
+    // device buffers (persistent: grown on demand, reused by later layouts, freed at destroy)
     void *xs = nullptr;
     uint32_t *perm = nullptr;
     void *lab = nullptr;             // sorted-order labels: uint16 when k <= 65535, else int32
@@ -61,7 +62,7 @@ struct pcm_engine {
     int32_t *fc_lab = nullptr;
     float4 *C = nullptr, *Cn = nullptr;
     unsigned long long *prev = nullptr;        // raw statistics of the previous iteration
-    double *scratch_d = nullptr;
+    int iscale = 0;                  // exact-inertia weight exponent (from the global q)
     unsigned long long *partials = nullptr, *stats = nullptr, *hist_changed = nullptr;
     unsigned long long *stats_own = nullptr;   // engine-owned; `stats` may point at a bound buffer
     unsigned long long *held = nullptr;        // statistics of a halted iteration
@@ -74,6 +75,9 @@ struct pcm_engine {
     int *rank_buf = nullptr;
     int rank_cap = 0;
     int *empty_idx = nullptr;        // [K] scratch of the relocation kernel
+    uint32_t *ntiles_dev = nullptr;  // tile count of the current layout (written by k_tile_total)
+    size_t cap_xs = 0, cap_lab = 0, cap_perm = 0, cap_cells = 0, cap_fc = 0, cap_tiles = 0, cap_ws = 0;
+    void *ws = nullptr;              // layout / relocation scratch arena
     Ctrl ctrl_host{};
     // optional kernel timing: event pairs per iteration, summed on read
     static constexpr int TEV = 64;
@@ -131,16 +135,44 @@ int dispatch_l(const pcm_engine *e, F &&f) {
     return f(int32_t{});
 }
 
+// The layout's buffers persist across layouts (a later cloud reuses them when
+// they are large enough); invalidating a layout frees nothing.
 void free_layout(pcm_engine *e) {
-    void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off};
-    for (void *p : ps)
-        if (p) (void)hipFree(p);
-    e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
-    e->tile_off = nullptr;
-    e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
     e->layout_ready = false;
     e->fit_ready = false;
 }
+
+void free_buffers(pcm_engine *e) {
+    void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->ws};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
+    e->tile_off = nullptr; e->ws = nullptr;
+    e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
+    e->cap_xs = e->cap_lab = e->cap_perm = e->cap_cells = e->cap_fc = e->cap_tiles = e->cap_ws = 0;
+    free_layout(e);
+}
+
+// Grow-only device buffer: reallocates (after freeing the old one) only when
+// `need` bytes exceed the capacity.
+template <typename P>
+hipError_t ensure(P *&p, size_t &cap, size_t need) {
+    if (p && need <= cap) return hipSuccess;
+    if (p) {
+        hipError_t err = hipFree((void *)p);
+        p = nullptr;
+        cap = 0;
+        if (err != hipSuccess) return err;
+    }
+    void *q = nullptr;
+    hipError_t err = hipMalloc(&q, std::max<size_t>(need, 256));
+    if (err != hipSuccess) return err;
+    p = static_cast<P *>(q);
+    cap = std::max<size_t>(need, 256);
+    return hipSuccess;
+}
+
+size_t align_up(size_t v, size_t a = 256) { return (v + a - 1) / a * a; }
 
 // Choose the pruning grid: about min(32 K, n / 2800) roughly cubic cells over
 // the bounding box (degenerate axes get one cell).
@@ -206,11 +238,31 @@ void choose_grid(pcm_engine *e) {
 
 int blocks_for(long long n, int bs = 256) { return (int)std::max(1LL, (n + bs - 1) / bs); }
 
+// Exact-inertia exponent s (oracle/lloyd_ref.py inertia_scale): the global
+// exponents give |x_a|, |c_a| < 2^(QBITS - q_a), so every canonical distance
+// is below bound = sum_a 4^(QBITS + 1 - q_a) (times 1 + 2^-20 for rounding);
+// s = 64 - e with bound' < 2^e keeps trunc(d * 2^s) < 2^64.
+int inertia_scale(const int32_t *q, int d) {
+    double bound = 0.0;
+    for (int a = 0; a < d; ++a) bound += std::ldexp(1.0, 2 * (QBITS + 1 - q[a]));
+    int e = 0;
+    (void)std::frexp(bound * (1.0 + std::ldexp(1.0, -20)), &e);
+    return 64 - e;
+}
+
 }  // namespace
 
 extern "C" {
 
 int pcm_abi_version(void) { return PCM_ABI_VERSION; }
+
+double pcm_inertia_value(const uint64_t *limbs, int scale, uint32_t overflow) {
+    if (!limbs) return 0.0;
+    if (overflow) return HUGE_VAL;
+    const unsigned __int128 v = (unsigned __int128)limbs[0] + ((unsigned __int128)limbs[1] << 32) +
+                                ((unsigned __int128)limbs[2] << 64);
+    return std::ldexp((double)v, -scale);   // one correctly rounded conversion, exact scaling
+}
 
 int pcm_last_error(char *buf, size_t n) {
     if (!buf || n == 0) return PCM_E_ARG;
@@ -241,7 +293,6 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->C, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->prev, nstat * sizeof(unsigned long long));
-    err = err ? err : hipMalloc(&e->scratch_d, sizeof(double));
     err = err ? err : hipMalloc(&e->partials, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
     e->stats = e->stats_own;
@@ -254,6 +305,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->bbox_out, 2 * MAXD * sizeof(double));
     err = err ? err : hipMalloc(&e->cand_stats, 3 * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->empty_idx, (size_t)k * sizeof(int));
+    err = err ? err : hipMalloc(&e->ntiles_dev, 2 * sizeof(uint32_t));
     err = err ? err : hipMemset(e->partials, 0, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMemset(e->ctrl, 0, sizeof(Ctrl));
     if (err != hipSuccess) {
@@ -269,9 +321,9 @@ int pcm_engine_destroy(pcm_engine *e) {
     for (int i = 0; i < pcm_engine::TEV; ++i)
         for (int j = 0; j < 4; ++j)
             if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
-    free_layout(e);
-    void *ps[] = {e->C, e->Cn, e->prev, e->scratch_d, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
-                  e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx};
+    free_buffers(e);
+    void *ps[] = {e->C, e->Cn, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
+                  e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx, e->ntiles_dev};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -325,6 +377,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     hipStream_t s = (hipStream_t)stream;
     free_layout(e);
     for (int a = 0; a < MAXD; ++a) e->qe.q[a] = a < e->d ? q[a] : 0;
+    e->iscale = inertia_scale(q, e->d);
     e->gidx0 = gidx0;
     const long long n = e->n;
     e->npad = ((n + 3) / 4) * 4 + 4;
@@ -334,121 +387,96 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     choose_grid(e);
     const long long nc = e->g.ncells;
     const size_t ts = tsize(e->dtype);
+    // every cell holds ceil(count / TILE) <= count / TILE + 1 tiles
+    e->ntiles_cap = nc + n / TILE + 1;
+    e->ntiles = -1;
 
-    HIPCHK(hipMalloc(&e->xs, (size_t)e->d * e->npad * ts));
-    HIPCHK(hipMalloc(&e->lab, (size_t)e->npad * lsize(e)));
-    HIPCHK(hipMalloc(&e->perm, (size_t)std::max(1LL, n) * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->cell_start, (size_t)(nc + 1) * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->fc_cnt, (size_t)nc * sizeof(uint32_t)));
-    // candidate lists [ncells][CAPF]
-    HIPCHK(hipMalloc(&e->fc_rec, (size_t)nc * CAPF * sizeof(float4)));
-    HIPCHK(hipMalloc(&e->fc_lab, (size_t)nc * CAPF * sizeof(int32_t)));
+    // persistent layout buffers (no allocation when an earlier layout was as large)
+    HIPCHK(ensure(e->xs, e->cap_xs, (size_t)e->d * e->npad * ts));
+    HIPCHK(ensure(e->lab, e->cap_lab, (size_t)e->npad * lsize(e)));
+    HIPCHK(ensure(e->perm, e->cap_perm, (size_t)std::max(1LL, n) * sizeof(uint32_t)));
+    {
+        // cell_start, tile_off: nc + 1 each; fc_cnt: nc -- one grow-only allocation each
+        size_t need = (size_t)(nc + 1) * sizeof(uint32_t);
+        size_t c0 = e->cap_cells, c1 = e->cap_cells;
+        HIPCHK(ensure(e->cell_start, c0, need));
+        HIPCHK(ensure(e->tile_off, c1, need));
+        size_t c2 = e->cap_cells;
+        HIPCHK(ensure(e->fc_cnt, c2, need));
+        e->cap_cells = std::min(c0, std::min(c1, c2));
+        size_t f0 = e->cap_fc, f1 = e->cap_fc;
+        HIPCHK(ensure(e->fc_rec, f0, (size_t)nc * CAPF * sizeof(float4)));
+        HIPCHK(ensure(e->fc_lab, f1, (size_t)nc * CAPF * sizeof(float4)));   // sized like fc_rec: one capacity
+        e->cap_fc = std::min(f0, f1);
+    }
+    HIPCHK(ensure(e->tiles, e->cap_tiles, (size_t)e->ntiles_cap * sizeof(uint4)));
     HIPCHK(hipMemsetAsync(e->fc_rec, 0, (size_t)nc * CAPF * sizeof(float4), s));
     HIPCHK(hipMemsetAsync(e->fc_lab, 0, (size_t)nc * CAPF * sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(e->fc_cnt, 0, (size_t)nc * sizeof(uint32_t), s));
 
     if (n == 0) {
-        HIPCHK(hipMalloc(&e->tile_off, (size_t)(nc + 1) * sizeof(uint32_t)));
         HIPCHK(hipMemsetAsync(e->tile_off, 0, (size_t)(nc + 1) * sizeof(uint32_t), s));
         HIPCHK(hipMemsetAsync(e->cell_start, 0, (size_t)(nc + 1) * sizeof(uint32_t), s));
         HIPCHK(hipMemsetAsync(e->lab, 0xff, (size_t)e->npad * lsize(e), s));
         HIPCHK(hipMemsetAsync(e->xs, 0, (size_t)e->d * e->npad * ts, s));
+        HIPCHK(hipMemsetAsync(e->ntiles_dev, 0, sizeof(uint32_t), s));
         e->ntiles = 0;
-        HIPCHK(hipStreamSynchronize(s));
+        e->ntiles_cap = 0;
         e->layout_ready = true;
         return 0;
     }
 
-    uint32_t *keys = nullptr, *keys2 = nullptr, *vals = nullptr, *tcnt = nullptr;
-    void *tmp = nullptr;
-    size_t tmp_bytes = 0, scan_bytes = 0;
-    auto cleanup = [&]() {
-        void *ps[] = {keys, keys2, vals, tcnt, tmp};
-        for (void *p : ps)
-            if (p) (void)hipFree(p);
-    };
-    int rc = 0;
-    do {
-        hipError_t err;
-        if ((err = hipMalloc(&keys, n * sizeof(uint32_t))) || (err = hipMalloc(&keys2, n * sizeof(uint32_t))) ||
-            (err = hipMalloc(&vals, n * sizeof(uint32_t))) || (err = hipMalloc(&tcnt, nc * sizeof(uint32_t))) ||
-            (err = hipMalloc(&e->tile_off, (nc + 1) * sizeof(uint32_t)))) {
-            rc = fail(PCM_E_NOMEM, std::string("layout scratch: ") + hipGetErrorString(err));
-            break;
-        }
-        unsigned bits = 1;
-        while ((1LL << bits) < nc) ++bits;
-        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-            using TT = decltype(T);
-            constexpr int D = decltype(DD)::value;
-            k_cellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, keys, vals);
-            LAUNCHCHK();
-            return 0;
-        });
-        if (rc) break;
-        if ((err = rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))) {
-            rc = fail(PCM_E_HIP, "radix_sort size query failed");
-            break;
-        }
-        uint32_t *toff = e->tile_off;
-        if ((err = rocprim::exclusive_scan(nullptr, scan_bytes, tcnt, toff, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s))) {
-            rc = fail(PCM_E_HIP, "scan size query failed");
-            break;
-        }
-        if ((err = hipMalloc(&tmp, std::max(tmp_bytes, scan_bytes)))) {
-            rc = fail(PCM_E_NOMEM, "sort scratch");
-            break;
-        }
-        size_t tb = tmp_bytes;
-        if ((err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))) {
-            rc = fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
-            break;
-        }
-        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-            using TT = decltype(T);
-            constexpr int D = decltype(DD)::value;
-            k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs);
-            LAUNCHCHK();
-            return 0;
-        });
-        if (rc) break;
-        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, e->cell_start);
-        if ((err = hipGetLastError())) { rc = fail(PCM_E_HIP, "k_cell_starts"); break; }
-        k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt);
-        if ((err = hipGetLastError())) { rc = fail(PCM_E_HIP, "k_tile_counts"); break; }
-        size_t sb = scan_bytes;
-        if ((err = rocprim::exclusive_scan(tmp, sb, tcnt, toff, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s))) {
-            rc = fail(PCM_E_HIP, "scan");
-            break;
-        }
-        uint32_t last_off = 0, last_cnt = 0;
-        if ((err = hipMemcpyAsync(&last_off, toff + nc - 1, 4, hipMemcpyDeviceToHost, s)) ||
-            (err = hipMemcpyAsync(&last_cnt, tcnt + nc - 1, 4, hipMemcpyDeviceToHost, s)) ||
-            (err = hipStreamSynchronize(s))) {
-            rc = fail(PCM_E_HIP, std::string("tile count readback: ") + hipGetErrorString(err));
-            break;
-        }
-        e->ntiles = (long long)last_off + last_cnt;
-        {
-            uint32_t nt32 = (uint32_t)e->ntiles;
-            if ((err = hipMemcpy(toff + nc, &nt32, 4, hipMemcpyHostToDevice))) {
-                rc = fail(PCM_E_HIP, "tile_off tail");
-                break;
-            }
-        }
-        if ((err = hipMalloc(&e->tiles, (size_t)std::max(1LL, e->ntiles) * sizeof(uint4)))) {
-            rc = fail(PCM_E_NOMEM, "tiles");
-            break;
-        }
-        k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, toff, nc, e->tiles);
-        if ((err = hipGetLastError())) { rc = fail(PCM_E_HIP, "k_tile_write"); break; }
-        if ((err = hipStreamSynchronize(s))) { rc = fail(PCM_E_HIP, std::string("layout: ") + hipGetErrorString(err)); break; }
-    } while (0);
-    cleanup();
-    if (rc) {
-        free_layout(e);
-        return rc;
-    }
+    // scratch arena: keys, sorted keys, values (u32 n each), tile counts (nc), rocprim temp
+    unsigned bits = 1;
+    while ((1LL << bits) < nc) ++bits;
+    size_t sort_bytes = 0, scan_bytes = 0;
+    if (rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (uint32_t *)nullptr, (size_t)n, 0u, bits, s) != hipSuccess ||
+        rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)nc,
+                                rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return fail(PCM_E_HIP, "layout: rocprim size query failed");
+    const size_t o_keys = 0, o_keys2 = align_up(o_keys + n * 4), o_vals = align_up(o_keys2 + n * 4),
+                 o_tcnt = align_up(o_vals + n * 4), o_tmp = align_up(o_tcnt + nc * 4),
+                 ws_need = o_tmp + std::max(sort_bytes, scan_bytes);
+    if (ensure(e->ws, e->cap_ws, ws_need) != hipSuccess) return fail(PCM_E_NOMEM, "layout scratch");
+    char *wb = (char *)e->ws;
+    uint32_t *keys = (uint32_t *)(wb + o_keys), *keys2 = (uint32_t *)(wb + o_keys2), *vals = (uint32_t *)(wb + o_vals),
+             *tcnt = (uint32_t *)(wb + o_tcnt);
+    void *tmp = wb + o_tmp;
+
+    int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        k_cellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, keys, vals);
+        LAUNCHCHK();
+        return 0;
+    });
+    if (rc) return rc;
+    size_t tb = sort_bytes;
+    if (hipError_t err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))
+        return fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
+    rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        k_gather<TT, D><<<blocks_for((e->npad + GATHER_PER - 1) / GATHER_PER), 256, 0, s>>>((const TT *)X, n, e->npad,
+                                                                                          e->perm, (TT *)e->xs);
+        LAUNCHCHK();
+        return 0;
+    });
+    if (rc) return rc;
+    k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, e->cell_start);
+    LAUNCHCHK();
+    k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt);
+    LAUNCHCHK();
+    size_t sb = scan_bytes;
+    if (rocprim::exclusive_scan(tmp, sb, tcnt, e->tile_off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return fail(PCM_E_HIP, "layout: tile scan");
+    k_tile_total<<<1, 64, 0, s>>>(e->tile_off, tcnt, nc, e->ntiles_dev);
+    LAUNCHCHK();
+    k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles);
+    LAUNCHCHK();
+    // stream-ordered: no host synchronisation (work queued later on `stream`
+    // sees the layout; X must not be modified by other streams meanwhile)
     e->layout_ready = true;
     return 0;
 }
@@ -512,7 +540,7 @@ static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, TPB, lds) != hipSuccess || per_cu < 1)
         per_cu = 2;
     if (const char *ov = std::getenv("PCM_ASSIGN_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(ov));
-    return (int)std::min<long long>(e->ntiles, (long long)per_cu * e->num_cu);
+    return (int)std::max(1LL, std::min<long long>(e->ntiles_cap, (long long)per_cu * e->num_cu));
 }
 
 static LloydArgs lloyd_args(pcm_engine *e) {
@@ -520,7 +548,7 @@ static LloydArgs lloyd_args(pcm_engine *e) {
     A.xs = e->xs;
     A.npad = e->npad;
     A.tiles = e->tiles;
-    A.ntiles = e->ntiles;
+    A.ntiles = e->ntiles_dev;
     A.fc_rec = e->fc_rec;
     A.fc_lab = e->fc_lab;
     A.C = e->C;
@@ -533,17 +561,18 @@ static LloydArgs lloyd_args(pcm_engine *e) {
 }
 
 // E-step with the current centres: candidate lists, then labels (sorted
-// order, e->lab) and the inertia added into *inert.  Not gated.
-static int launch_labels(pcm_engine *e, hipStream_t s, double *inert) {
+// order, e->lab) and, when inert is non-null, the exact inertia limbs added
+// into inert[0..3].  Not gated.
+static int launch_labels(pcm_engine *e, hipStream_t s, unsigned long long *inert) {
     if (int rc = launch_candidates(e, s, 0)) return rc;
     LloydArgs A = lloyd_args(e);
     return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
-        if (e->ntiles == 0) return 0;
+        if (e->n == 0) return 0;
         return dispatch_l(e, [&](auto L) -> int {
             using LT = decltype(L);
-            k_label<TT, D, LT><<<assign_grid(e, (const void *)k_label<TT, D, LT>, 0), TPB, 0, s>>>(A, e->lab, inert);
+            k_label<TT, D, LT><<<assign_grid(e, (const void *)k_label<TT, D, LT>, 0), TPB, 0, s>>>(A, e->lab, inert, e->iscale);
             LAUNCHCHK();
             return 0;
         });
@@ -595,7 +624,7 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool fold) {
     return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
-        if (e->ntiles > 0) {
+        if (e->n > 0) {
             const size_t lds = (size_t)AccL<D>::words * sizeof(uint32_t);
             k_lloyd<TT, D><<<assign_grid(e, (const void *)k_lloyd<TT, D>, lds), TPB, lds, s>>>(A, e->tiles, e->fc_rec,
                                                                                               e->fc_lab, e->C, e->fc_cnt);
@@ -711,7 +740,7 @@ int pcm_reloc_candidates(pcm_engine *e, int m, void *records, void *stream) {
             break;
         }
         // labels of the halted iteration (the iterations keep no label array)
-        if ((rc = launch_labels(e, s, e->scratch_d))) break;
+        if ((rc = launch_labels(e, s, nullptr))) break;
         rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
             using TT = decltype(T);
             constexpr int D = decltype(DD)::value;
@@ -779,8 +808,8 @@ int pcm_final(pcm_engine *e, void *stream) {
     if (!e) return fail(PCM_E_ARG, "null engine");
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipMemsetAsync(&e->ctrl->inertia, 0, sizeof(double), s));
-    return launch_labels(e, s, &e->ctrl->inertia);
+    HIPCHK(hipMemsetAsync(e->ctrl->inert, 0, sizeof(e->ctrl->inert), s));
+    return launch_labels(e, s, e->ctrl->inert);
 }
 
 int pcm_labels(pcm_engine *e, int32_t *out, void *stream) {
@@ -826,7 +855,10 @@ int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream) {
     out->done = h.done;
     out->iter = h.iter;
     out->n_empty = h.n_empty;
-    out->inertia = h.inertia;
+    for (int q = 0; q < 3; ++q) out->inertia_limbs[q] = h.inert[q];
+    out->inertia_scale = e->iscale;
+    out->inertia_overflow = (uint32_t)h.inert[3];
+    out->inertia = pcm_inertia_value(out->inertia_limbs, e->iscale, out->inertia_overflow);
     out->last_changed = h.last_changed;
     out->last_shift = h.last_shift;
     return 0;
@@ -835,6 +867,11 @@ int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream) {
 int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid) {
     if (!e || !ncells || !ntiles || !grid) return fail(PCM_E_ARG, "bad argument");
     *ncells = e->g.ncells;
+    if (e->layout_ready && e->ntiles < 0) {   // read back lazily (synchronises the device)
+        uint32_t nt = 0;
+        HIPCHK(hipMemcpy(&nt, e->ntiles_dev, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        e->ntiles = nt;
+    }
     *ntiles = e->ntiles;
     for (int a = 0; a < MAXD; ++a) grid[a] = e->g.G[a];
     return 0;

@@ -51,7 +51,7 @@ struct Ctrl {
     uint32_t halt, done, iter, max_iter;
     uint32_t n_empty, resume, status, pad0;
     double tol;
-    double inertia;
+    unsigned long long inert[4];    // exact inertia: 32-bit limbs of sum trunc(d * 2^s), [3] = overflow count
     unsigned long long neq_saved;   // stat words changed at a halted iteration (used on resume)
     unsigned long long last_changed;
     double last_shift;
@@ -224,18 +224,28 @@ __global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long lo
     vals[i] = (uint32_t)i;
 }
 
-// SoA gather into cell order; labels := -1
+// AoS gather into cell order: GATHER_PER consecutive destination rows per
+// thread (their perm entries loaded at once), so every thread keeps
+// GATHER_PER * D independent random reads in flight.
+constexpr int GATHER_PER = 1;   // 4 measured slower (3.06 vs 2.5 ms at 100M): random 12-B rows are HBM-line bound
 template <typename T, int D>
 __global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long long n, long long npad,
                                                 const uint32_t *__restrict__ perm, T *__restrict__ xs) {
-    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= npad) return;
-    if (i < n) {
-        long long s = perm[i];
-        for (int a = 0; a < D; ++a) xs[i * D + a] = X[s * D + a];
-    } else {
-        for (int a = 0; a < D; ++a) xs[i * D + a] = (T)0.0f;
-    }
+    const long long i0 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * GATHER_PER;
+    if (i0 >= npad) return;
+    long long src[GATHER_PER];
+#pragma unroll
+    for (int e = 0; e < GATHER_PER; ++e) src[e] = (i0 + e < n) ? (long long)perm[i0 + e] : -1;
+    T v[GATHER_PER][D];
+#pragma unroll
+    for (int e = 0; e < GATHER_PER; ++e)
+#pragma unroll
+        for (int a = 0; a < D; ++a) v[e][a] = src[e] >= 0 ? X[src[e] * D + a] : (T)0.0f;
+#pragma unroll
+    for (int e = 0; e < GATHER_PER; ++e)
+        if (i0 + e < npad)
+#pragma unroll
+            for (int a = 0; a < D; ++a) xs[(i0 + e) * D + a] = v[e][a];
 }
 
 // cell_start[c] = first sorted index with key >= c, for c in [0, ncells]
@@ -254,6 +264,15 @@ __global__ __launch_bounds__(256) void k_tile_counts(const uint32_t *__restrict_
     if (c >= ncells) return;
     uint32_t n = start[c + 1] - start[c];
     cnt[c] = (n + TILE - 1) / TILE;
+}
+
+// tile_off[nc] and the tile count (the scan is exclusive: add the last cell's count)
+__global__ void k_tile_total(uint32_t *__restrict__ off, const uint32_t *__restrict__ cnt, long long ncells,
+                             uint32_t *__restrict__ ntiles) {
+    if (threadIdx.x != 0) return;
+    const uint32_t t = off[ncells - 1] + cnt[ncells - 1];
+    off[ncells] = t;
+    *ntiles = t;
 }
 
 __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__ start, const uint32_t *__restrict__ off,
@@ -638,7 +657,7 @@ struct LloydArgs {
     long long npad;
     const uint4 *tiles;             // {cell, start, end, -}
     const uint32_t *fc_cnt;         // candidate count per cell (FULL: all K)
-    long long ntiles;
+    const uint32_t *ntiles;         // device: tile count of the layout
     const float4 *fc_rec;
     const int32_t *fc_lab;
     const float4 *C;                // all centres (FULL cells)
@@ -667,22 +686,53 @@ __device__ __forceinline__ TileL make_tile(const uint4 &t, int K) {
     return h;
 }
 
+// Exact, order-independent inertia: a point adds w = trunc(d * 2^s) (d the
+// canonical fp32 distance; s from the global fixed-point exponents so that
+// w < 2^64, see inertia_scale); per-thread 128-bit sums are split into three
+// 32-bit limbs, which are summed with integer atomics.  The total is the same
+// integer for any block order, grid size or number of ranks
+// (oracle/lloyd_ref.py inertia_exact).
+__device__ __forceinline__ void inert_add(unsigned long long &lo, unsigned long long &hi, unsigned &ovf, float d,
+                                          int s) {
+    const double v = __builtin_ldexp((double)d, s);
+    unsigned long long w;
+    if (v < 18446744073709551616.0) {
+        w = (unsigned long long)v;   // truncation (d >= 0)
+    } else {
+        w = ~0ull;
+        ++ovf;
+    }
+    lo += w;
+    hi += (lo < w) ? 1ull : 0ull;
+}
+
+__device__ __forceinline__ void inert_flush(unsigned long long lo, unsigned long long hi, unsigned ovf,
+                                            unsigned long long *__restrict__ out) {
+    unsigned long long l[4] = {lo & 0xffffffffull, lo >> 32, hi, (unsigned long long)ovf};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        for (int o = 32; o > 0; o >>= 1) l[q] += __shfl_xor(l[q], o);
+        if ((threadIdx.x & 63) == 0 && l[q]) atomicAdd(out + q, l[q]);
+    }
+}
+
 // E-step with the current centres writing labels (sorted order) and the
 // inertia (final E-step of _kmeans.py:736-750, relocation keys).  Not gated.
 // Same tile walk and candidate lists as k_lloyd; 4 points per lane per round,
 // the loads of the next round in flight while one is computed.
 template <typename T, int D, typename LT>
-__global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, double *inert_out) {
+__global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned long long *inert_out, int iscale) {
     __shared__ float4 crec[CAPF];
     __shared__ int32_t cid[CAPF];
     const int tid = threadIdx.x;
     const unsigned G = gridDim.x;
-    const unsigned nt = (unsigned)A.ntiles;
+    const unsigned nt = *A.ntiles;
     const float4 *lrec = A.fc_rec;
     const int32_t *llab = A.fc_lab;
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     const rsrc_t rl = make_rsrc(lab, (unsigned long long)A.npad * sizeof(LT));
-    double inert = 0.0;
+    unsigned long long ilo = 0ull, ihi = 0ull;
+    unsigned iovf = 0u;
     for (unsigned t = blockIdx.x; t < nt; t += G) {
         uint4 tr = A.tiles[t];
         tr.w = A.fc_cnt[tr.x];
@@ -709,14 +759,13 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, double *i
             for (int e = 0; e < 4; ++e) {
                 lbl[e] = h.full ? bj[e] : cid[bj[e]];
                 v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
-                if (v[e]) inert += (double)bd[e];
+                if (v[e] && inert_out) inert_add(ilo, ihi, iovf, bd[e], iscale);
             }
             if (i0 < h.end) store_l4(rl, i0, lbl, v, (RawLab<LT> *)nullptr);
             cur = nxt;
         }
     }
-    for (int o = 32; o > 0; o >>= 1) inert += __shfl_xor(inert, o);
-    if ((tid & 63) == 0) atomicAdd(inert_out, inert);
+    if (inert_out) inert_flush(ilo, ihi, iovf, inert_out);
 }
 
 // ------------------------------------------------------------------ Lloyd iteration
@@ -778,7 +827,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     __shared__ int32_t cid[2][CAPF];
     const int tid = threadIdx.x;
     const unsigned G = gridDim.x;
-    const unsigned nt = (unsigned)A.ntiles;
+    const unsigned nt = *A.ntiles;
     unsigned t = blockIdx.x;
     if (t >= nt) return;
     const float4 *lrec = fc_rec;

@@ -117,7 +117,9 @@ class Engine:
         st = _lib.PcmStatus()
         _lib.check(self.lib.pcm_read_status(self.h, ctypes.byref(st), _stream()), "pcm_read_status")
         return dict(halt=st.halt, done=st.done, iter=st.iter, n_empty=st.n_empty, inertia=st.inertia,
-                    last_changed=st.last_changed, last_shift=st.last_shift)
+                    last_changed=st.last_changed, last_shift=st.last_shift,
+                    inertia_limbs=[int(v) for v in st.inertia_limbs], inertia_scale=int(st.inertia_scale),
+                    inertia_overflow=int(st.inertia_overflow))
 
     def reloc_candidates(self, m: int) -> torch.Tensor:
         rec = torch.zeros(m * RELOC_RECORD_BYTES, dtype=torch.uint8, device=self.device)

@@ -21,3 +21,13 @@ def fixed_q(maxabs) -> list:
         e = 0 if m == 0.0 else math.frexp(m)[1]
         out.append(QBITS - e)
     return out
+
+
+def inertia_from_limbs(limbs, scale: int, overflow: int = 0) -> float:
+    """Global inertia from the (all-reduced) exact limbs of pcm_status:
+    ``ldexp(float(l0 + l1 * 2**32 + l2 * 2**64), -scale)`` -- Python's int -> float
+    conversion rounds once to nearest, like ``pcm_inertia_value``."""
+    if overflow:
+        return math.inf
+    total = int(limbs[0]) + (int(limbs[1]) << 32) + (int(limbs[2]) << 64)
+    return math.ldexp(float(total), -int(scale))

@@ -26,7 +26,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from .fixed import fixed_q
+from .fixed import fixed_q, inertia_from_limbs
 
 
 @dataclass
@@ -128,10 +128,12 @@ def finish(engine, group=None):
     engine.final()
     st = engine.status()
     inertia = st["inertia"]
-    if world > 1:
-        t = torch.tensor([inertia], dtype=torch.float64, device=engine.stats_device)
+    if world > 1:   # exact integer limbs: the same inertia for any world size
+        t = torch.tensor(list(st["inertia_limbs"]) + [st["inertia_overflow"]], dtype=torch.int64,
+                         device=engine.stats_device)
         dist.all_reduce(t, group=group)
-        inertia = float(t.item())
+        v = [int(x) for x in t.cpu().tolist()]
+        inertia = inertia_from_limbs(v[:3], st["inertia_scale"], v[3])
     return engine.labels(), engine.centers(), inertia
 
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PCM_ABI_VERSION 1
+#define PCM_ABI_VERSION 2
 
 enum pcm_dtype { PCM_F32 = 0, PCM_F16 = 1 };
 
@@ -57,14 +57,25 @@ typedef struct pcm_status {
     uint32_t done;       /* 0 running, 1 strict label convergence, 2 shift<=tol, 3 max_iter */
     uint32_t iter;       /* completed Lloyd iterations */
     uint32_t n_empty;    /* empty clusters seen by the halted iteration */
-    double inertia;      /* local inertia of the last pcm_final */
+    double inertia;      /* local inertia of the last pcm_final (= pcm_inertia_value of the fields below) */
     uint64_t last_changed;
     double last_shift;
+    /* Exact, order-independent inertia: sum over points of trunc(d * 2^scale)
+     * (d = canonical fp32 distance to the final centre) as 32-bit limbs
+     * inertia_limbs[0] + 2^32 [1] + 2^64 [2].  Sum-all-reduce the limbs over
+     * ranks, then pcm_inertia_value gives the global inertia; the result is
+     * bit-identical for any world size. */
+    uint64_t inertia_limbs[3];
+    int32_t inertia_scale;
+    uint32_t inertia_overflow;   /* > 0: a distance exceeded the bound (inertia = +inf) */
 } pcm_status;
 
 typedef struct pcm_engine pcm_engine;
 
 int pcm_abi_version(void);
+/* Inertia from (all-reduced) limbs: ldexp((double)(l0 + l1 2^32 + l2 2^64), -scale),
+ * one correctly rounded conversion; +inf when overflow > 0. */
+double pcm_inertia_value(const uint64_t *limbs, int scale, uint32_t overflow);
 int pcm_last_error(char *buf, size_t n);
 
 /* Create an engine for D-dimensional points (1..4), K clusters, on HIP device

@@ -39,7 +39,12 @@ so that labels can be bit-exact between CPU and GPU:
   still empty afterwards copies the (averaged) centre of the first
   largest cluster;
 * shift: ``sum_j sum_a (c_new - c_old)**2`` in float64 with the fixed reduction
-  tree of the GPU finalize kernel (1024 sequential lanes, then halving).
+  tree of the GPU finalize kernel (1024 sequential lanes, then halving);
+* inertia (``_kmeans.py:750``, sklearn's ``_inertia_dense``): the exact integer
+  ``sum_i trunc(d_i * 2**s)`` of the canonical float32 distances, ``s`` from the
+  global fixed-point exponents (``inertia_scale``), converted to float64 once
+  and scaled by ``2**-s`` -- independent of summation order, block count and
+  world size (sklearn's float32/float64 sum depends on its thread count).
 
 Parity status: pinned against scikit-learn golden vectors generated in the
 build container (``tests/golden/make_golden.py``) and against the
@@ -47,6 +52,8 @@ hand-computed sklearn known-answer tests restated as numbers in
 ``tests/test_oracle_golden.py``.
 """
 from __future__ import annotations
+
+import math
 
 import numpy as np
 
@@ -237,11 +244,31 @@ def shift_total(Cn, Co) -> float:
     return float(acc[0])
 
 
-def inertia(X, C, labels, weights=None) -> float:
-    d = sqdist_rows(X, C[labels]).astype(np.float64)
-    if weights is not None:
-        d = d * np.asarray(weights, dtype=np.float64)
-    return float(d.sum())
+def inertia_scale(q) -> int:
+    """Exponent s with trunc(d * 2**s) < 2**64 for every canonical distance d:
+    |x_a|, |c_a| < 2**(QBITS - q_a) bound d by sum_a 4**(QBITS + 1 - q_a)
+    (times 1 + 2**-20 for the float32 rounding)."""
+    bound = sum(math.ldexp(1.0, 2 * (QBITS + 1 - int(qa))) for qa in q)
+    _, e = math.frexp(bound * (1.0 + 2.0 ** -20))
+    return 64 - e
+
+
+def inertia_exact(d: np.ndarray, s: int) -> float:
+    """``ldexp(float(sum trunc(d * 2**s)), -s)`` with the sum an exact integer."""
+    w = np.ldexp(np.asarray(d, dtype=np.float32).astype(np.float64), s)
+    if w.size and float(w.max()) >= 2.0 ** 64:
+        return math.inf
+    w = w.astype(np.uint64)
+    lo = int(np.sum(w & np.uint64(0xFFFFFFFF), dtype=np.uint64))
+    hi = int(np.sum(w >> np.uint64(32), dtype=np.uint64))
+    return math.ldexp(float(lo + (hi << 32)), -s)
+
+
+def inertia(X, C, labels, weights=None, q=None) -> float:
+    d = sqdist_rows(X, C[labels])
+    if weights is None:
+        return inertia_exact(d, inertia_scale(fixed_q(X) if q is None else q))
+    return float((d.astype(np.float64) * np.asarray(weights, dtype=np.float64)).sum())
 
 
 # ---------------------------------------------------------------- driver
@@ -300,7 +327,7 @@ def lloyd_fit(X, C0, max_iter=300, tol=0.0, weights=None, shards=1, history=Fals
             break
         labels_old = labels
     labels = assign_fast(X, C) if fast else assign(X, C)
-    out = dict(labels=labels, centers=C, inertia=inertia(X, C, labels, wt), n_iter=it + 1,
+    out = dict(labels=labels, centers=C, inertia=inertia(X, C, labels, wt, q), n_iter=it + 1,
                strict=strict, changed=changed, q=q)
     if history:
         out["history"] = hist

@@ -46,6 +46,7 @@ class OracleEngine:
         self.tol, self.max_iter = float(tol), int(max_iter)
         self.hist_changed, self.hist_shift = [], []
         self.inertia = 0.0
+        self.limbs = [0, 0, 0]
         self.prev = np.zeros(self.k * (self.d + 1), np.int64)   # raw statistics of the previous iteration
         self.neq_saved = 0
 
@@ -101,6 +102,7 @@ class OracleEngine:
 
     def status(self):
         return dict(halt=self.halt, done=self.done, iter=self.it, n_empty=self.n_empty, inertia=self.inertia,
+                    inertia_limbs=list(self.limbs), inertia_scale=R.inertia_scale(self.q), inertia_overflow=0,
                     last_changed=self.hist_changed[-1] if self.hist_changed else 0,
                     last_shift=self.hist_shift[-1] if self.hist_shift else 0.0)
 
@@ -143,7 +145,12 @@ class OracleEngine:
     # ---------------- outputs
     def final(self):
         self.lab = R.assign(self.X, self.C)
-        self.inertia = R.inertia(self.X, self.C, self.lab) if self.n else 0.0
+        s = R.inertia_scale(self.q)
+        w = np.ldexp(R.sqdist_rows(self.X, self.C[self.lab]).astype(np.float64), s).astype(np.uint64)
+        lo = int(np.sum(w & np.uint64(0xFFFFFFFF), dtype=np.uint64))
+        hi = int(np.sum(w >> np.uint64(32), dtype=np.uint64))
+        self.limbs = [lo & 0xFFFFFFFF, (lo >> 32) + hi, 0]     # same integer as the device's limbs
+        self.inertia = R.inertia_exact(R.sqdist_rows(self.X, self.C[self.lab]), s) if self.n else 0.0
 
     def labels(self):
         return torch.from_numpy(self.lab.copy())

@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "pcm_kmeans.h")
 def declared():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\bint\s+(pcm_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(?:int|double)\s+(pcm_\w+)\s*\(", src)))
 
 
 @pytest.fixture(scope="module")
@@ -38,7 +38,8 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_abi_version(lib):
-    assert lib.pcm_abi_version() == 1
+    from pcm_amd import _lib
+    assert lib.pcm_abi_version() == _lib.ABI_VERSION
 
 
 def test_argument_errors_without_device(lib):
@@ -56,3 +57,12 @@ def test_no_fp_contraction_in_build_flags():
     from pcm_amd import _lib
     assert "-ffp-contract=off" in _lib.HIP_FLAGS
     assert "--offload-arch=gfx950" in _lib.HIP_FLAGS
+
+
+def test_inertia_value_from_limbs(lib):
+    """pcm_inertia_value: exact integer total, one rounding, exact scaling (host only)."""
+    import math
+    limbs = (ctypes.c_uint64 * 3)(0xFFFFFFFF, 0xFFFFFFFF, 12345)
+    total = 0xFFFFFFFF + (0xFFFFFFFF << 32) + (12345 << 64)
+    assert lib.pcm_inertia_value(limbs, 70, 0) == math.ldexp(float(total), -70)
+    assert lib.pcm_inertia_value(limbs, 0, 1) == float("inf")

@@ -68,7 +68,7 @@ def test_two_ranks_match_single_process(tmp_path, chunk):
         assert int(p["n_iter"]) == ref["n_iter"]
         # the engine reports changed statistic words, the oracle changed labels: zero together
         np.testing.assert_array_equal(np.asarray(p["changed"]) > 0, np.asarray(ref["changed"]) > 0)
-        assert float(p["inertia"]) == pytest.approx(ref["inertia"], rel=1e-12)
+        assert float(p["inertia"]) == ref["inertia"]
 
 
 def test_two_ranks_relocation(tmp_path):
@@ -99,4 +99,4 @@ def test_local_group_under_default_group(tmp_path):
     for p in parts:
         np.testing.assert_array_equal(p["labels"], ref["labels"])
         np.testing.assert_array_equal(p["centers"], ref["centers"])
-        assert float(p["inertia"]) == pytest.approx(ref["inertia"], rel=1e-12)
+        assert float(p["inertia"]) == ref["inertia"]

@@ -13,7 +13,7 @@ GPU box's host cores), on the same points:
   long candidate lists.
 
 Bar: labels bit-exact, centres bitwise equal, same n_iter, per-iteration
-change records zero together, inertia to 1e-9 relative.
+change records zero together, inertia bitwise equal (exact integer sum).
 """
 import numpy as np
 import pytest
@@ -43,7 +43,7 @@ def check(res, ref, where):
     assert bad.size == 0, f"{where}: {bad.size} labels differ, first rows {bad[:8]}"
     assert np.array_equal(cen, ref["centers"]), f"{where}: centres differ (max {np.abs(cen - ref['centers']).max()})"
     np.testing.assert_array_equal(res.changed > 0, np.asarray(ref["changed"], dtype=np.int64) > 0)
-    assert res.inertia == pytest.approx(ref["inertia"], rel=1e-9)
+    assert res.inertia == ref["inertia"]      # exact integer inertia: bitwise equal
 
 
 def device_cloud(pcm, n, d, dtype=torch.float32):

@@ -48,7 +48,7 @@ def assert_same(res, ref, where=""):
     assert np.array_equal(cen, ref["centers"]), f"{where} centres differ: max {np.abs(cen - ref['centers']).max()}"
     # the engine counts changed statistic words, the oracle changed labels: zero together
     np.testing.assert_array_equal(res.changed > 0, np.asarray(ref["changed"], dtype=np.int64) > 0)
-    assert res.inertia == pytest.approx(ref["inertia"], rel=1e-9, abs=1e-12)
+    assert res.inertia == ref["inertia"]      # exact integer inertia: bitwise equal
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))), ids=os.path.basename)
@@ -149,11 +149,13 @@ def test_relocation_many_empty(pcm):
 def test_tol_convergence(pcm):
     X = R.splitmix_uniform(40_000, 3, 14)
     C0 = X[R.init_indices(40_000, 50)]
-    ref = R.lloyd_fit(X, C0, max_iter=100, tol=1e-6, fast=True)
+    ref = R.lloyd_fit(X, C0, max_iter=100, tol=1e-6, fast=True, history=True)
     res = gpu_fit(pcm, X, C0, 100, tol=1e-6)
     assert not res.strict
     assert_same(res, ref, "tol")
-    np.testing.assert_array_equal(res.shift, np.array([h for h in res.shift]))
+    # per-iteration centre shifts: the same fixed fp64 reduction tree on both sides
+    np.testing.assert_array_equal(res.shift, np.array([h["shift"] for h in ref["history"]]))
+    assert res.shift[-1] <= 1e-6 < res.shift[-2]
 
 
 def test_bruteforce_operator(pcm):
