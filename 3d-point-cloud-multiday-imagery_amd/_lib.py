@@ -43,7 +43,8 @@ class PcmStatus(ctypes.Structure):
     _fields_ = [("halt", ctypes.c_uint32), ("done", ctypes.c_uint32), ("iter", ctypes.c_uint32),
                 ("n_empty", ctypes.c_uint32), ("inertia", ctypes.c_double), ("last_changed", ctypes.c_uint64),
                 ("last_shift", ctypes.c_double), ("inertia_limbs", ctypes.c_uint64 * 3),
-                ("inertia_scale", ctypes.c_int32), ("inertia_overflow", ctypes.c_uint32)]
+                ("inertia_scale", ctypes.c_int32), ("inertia_overflow", ctypes.c_uint32),
+                ("list_rebuilds", ctypes.c_uint32), ("pad_", ctypes.c_uint32)]
 
 
 def needs_build() -> bool:

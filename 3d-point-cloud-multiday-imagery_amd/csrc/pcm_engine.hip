@@ -61,6 +61,8 @@ struct pcm_engine {
     float4 *fc_rec = nullptr;
     int32_t *fc_lab = nullptr;
     float4 *C = nullptr, *Cn = nullptr;
+    float4 *cref = nullptr;                    // [2][K] reference centres of the candidate lists (k_step)
+    double drift_alpha = 2.0, drift_kappa = 0.05;  // candidate-list reuse policy (see k_step)
     unsigned long long *prev = nullptr;        // raw statistics of the previous iteration
     int iscale = 0;                  // exact-inertia weight exponent (from the global q)
     unsigned long long *partials = nullptr, *stats = nullptr, *hist_changed = nullptr;
@@ -292,6 +294,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     hipError_t err = hipSuccess;
     err = err ? err : hipMalloc(&e->C, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
+    err = err ? err : hipMalloc(&e->cref, (size_t)2 * k * sizeof(float4));
     err = err ? err : hipMalloc(&e->prev, nstat * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->partials, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
@@ -312,6 +315,10 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
         pcm_engine_destroy(e);
         return fail(PCM_E_NOMEM, std::string("engine allocation: ") + hipGetErrorString(err));
     }
+    // candidate-list reuse: budget = alpha x the last centre shift, at most kappa x
+    // the smallest cell width (tuning sweeps may override; alpha = 0 disables reuse)
+    if (const char *v = std::getenv("PCM_DRIFT_ALPHA")) e->drift_alpha = std::atof(v);
+    if (const char *v = std::getenv("PCM_DRIFT_KAPPA")) e->drift_kappa = std::atof(v);
     *out = e;
     return 0;
 }
@@ -322,7 +329,7 @@ int pcm_engine_destroy(pcm_engine *e) {
         for (int j = 0; j < 4; ++j)
             if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
     free_buffers(e);
-    void *ps[] = {e->C, e->Cn, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
+    void *ps[] = {e->C, e->Cn, e->cref, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
                   e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx, e->ntiles_dev};
     for (void *p : ps)
         if (p) (void)hipFree(p);
@@ -502,6 +509,7 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
     // as sklearn's labels-vs-(-1) comparison does
     HIPCHK(hipMemsetAsync(e->prev, 0, ((size_t)e->k * (e->d + 1) + 1) * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->partials, 0, (size_t)2 * e->k * (e->d + 1) * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(e->stats, 0, ((size_t)e->k * (e->d + 1) + 1) * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->hist_changed, 0, (size_t)e->max_iter_cap * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(e->hist_shift, 0, (size_t)e->max_iter_cap * sizeof(double), s));
     e->ctrl_host = Ctrl{};
@@ -527,7 +535,7 @@ static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
         constexpr int D = decltype(DD)::value;
         const int bpc = cand_bpc(e);
         k_cand<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
-                                                                 e->ctrl, gate, bpc);
+                                                                 e->ctrl, gate, bpc, e->cref);
         LAUNCHCHK();
         return 0;
     });
@@ -556,6 +564,7 @@ static LloydArgs lloyd_args(pcm_engine *e) {
     A.K = e->k;
     for (int a = 0; a < MAXD; ++a) A.q[a] = e->qe.q[a];
     A.partials = e->partials;
+    A.pstride = (long long)e->k * (e->d + 1);
     A.ctrl = e->ctrl;
     return A;
 }
@@ -615,12 +624,17 @@ static int timing_mark(pcm_engine *e, int which, hipStream_t s) {
 }
 
 // k_lloyd (its candidate lists were built by the previous k_step, the resume
-// path or pcm_fit_begin); with fold, k_fold copies partials[parity] into
-// `stats` (the all-reduce input) and zeroes it.
-static int iter_local_impl(pcm_engine *e, hipStream_t s, bool fold) {
+// path or pcm_fit_begin).  to_stats: accumulate straight into `stats` (the
+// all-reduce buffer, zeroed by the previous k_step / k_global / fit_begin);
+// otherwise into the single-GPU parity half partials[iter & 1].
+static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
     if (int rc = timing_mark(e, 0, s)) return rc;
     if (int rc = timing_mark(e, 1, s)) return rc;
     LloydArgs A = lloyd_args(e);
+    if (to_stats) {
+        A.partials = e->stats;
+        A.pstride = 0;
+    }
     return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
@@ -630,20 +644,14 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool fold) {
                                                                                               e->fc_lab, e->C, e->fc_cnt);
             LAUNCHCHK();
         }
-        if (int rc = timing_mark(e, 2, s)) return rc;
-        if (fold) {
-            const int nf = e->k * (D + 1) + 1;
-            k_fold<D><<<blocks_for(nf), 256, 0, s>>>(e->partials, e->k, e->stats, e->ctrl);
-            LAUNCHCHK();
-        }
-        return 0;
+        return timing_mark(e, 2, s);
     });
 }
 
 int pcm_iter_local(pcm_engine *e, void *stream) {
     if (!e) return fail(PCM_E_ARG, "null engine");
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
-    return iter_local_impl(e, (hipStream_t)stream, true);
+    return iter_local_impl(e, (hipStream_t)stream, true);   // into `stats`: the caller all-reduces it
 }
 
 // Centre update + next candidate lists.  stats_in: the all-reduced statistics
@@ -655,9 +663,20 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
         constexpr int D = decltype(DD)::value;
         if (e->k <= KSTEP_MAX && !resume_path) {
             const int bpc = cand_bpc(e);
-            k_step<D><<<(int)(e->g.ncoarse * bpc + 1), CAND_TPB, (size_t)e->k * sizeof(float4), s>>>(
-                e->g, from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C,
-                e->hist_changed, e->hist_shift, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab, bpc);
+            const size_t lds = (size_t)e->k * sizeof(float4);
+            static bool attr_set[MAXD + 1] = {false, false, false, false, false};
+            if (lds > 32768 && !attr_set[D]) {
+                HIPCHK(hipFuncSetAttribute((const void *)k_step<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(KSTEP_MAX * sizeof(float4))));
+                attr_set[D] = true;
+            }
+            double wmin = 0.0;
+            for (int a = 0; a < D; ++a)
+                if (e->g.ext[a] > 0 && (wmin == 0.0 || e->g.w[a] < wmin)) wmin = e->g.w[a];
+            k_step<D><<<(int)(e->g.ncoarse * bpc + 1), CAND_TPB, lds, s>>>(
+                e->g, from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->cref,
+                e->hist_changed, e->hist_shift, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab, bpc, e->drift_alpha,
+                e->drift_kappa * wmin);
             LAUNCHCHK();
             return 0;
         }
@@ -699,7 +718,7 @@ int pcm_iterate(pcm_engine *e, int n, void *stream) {
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
     hipStream_t s = (hipStream_t)stream;
     for (int i = 0; i < n; ++i) {
-        if (int rc = iter_local_impl(e, s, false)) return rc;
+        if (int rc = iter_local_impl(e, s, false)) return rc;   // parity halves of `partials`
         if (int rc = iter_global_impl(e, s, true, false)) return rc;
     }
     return 0;
@@ -859,6 +878,8 @@ int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream) {
     out->inertia_scale = e->iscale;
     out->inertia_overflow = (uint32_t)h.inert[3];
     out->inertia = pcm_inertia_value(out->inertia_limbs, e->iscale, out->inertia_overflow);
+    out->list_rebuilds = h.rebuilds;
+    out->pad_ = 0;
     out->last_changed = h.last_changed;
     out->last_shift = h.last_shift;
     return 0;

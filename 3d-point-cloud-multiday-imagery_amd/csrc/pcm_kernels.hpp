@@ -5,8 +5,6 @@
 //   k_lloyd            nearest centroid over the cell's candidates + LDS-privatised
 //                      fixed-point accumulation (replaces _k_means_lloyd.pyx:168-218)
 //   k_label            final E-step: labels + inertia (_kmeans.py:736-750)
-//   k_fold             replica fold of the partials (replaces the locked reduction
-//                      of _k_means_lloyd.pyx:142-152)
 //   k_global           averaging / shift / convergence (_k_means_common.pyx:274-311,
 //                      _kmeans.py:717-732)
 // Layout (once per cloud): k_bbox*, k_cellid, rocprim radix sort, k_gather,
@@ -28,12 +26,13 @@ constexpr int CAPF = 64;           // fine candidate capacity
 constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-centre ranks)
 constexpr int TPB = 256;           // assign block size
 constexpr int TILE = 8192;         // max points per tile (<= 63 per lane per flush)
-constexpr int KSTEP_MAX = 2048;    // k_step keeps the K new centres in LDS (<= 32 KB)
+constexpr int KSTEP_MAX = 4096;    // k_step keeps the K new centres in LDS (<= 64 KB of gfx950's 160 KB)
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int QBITS = 25;
 // Pruning margins (see DESIGN.md "Exactness of pruning").
 constexpr double PEPS = 7.62939453125e-06;   // 2^-17  >> 6 * 2^-24 (fp32 distance error)
 constexpr double PTAU = 1e-36;               // >> fp32 underflow error of a distance
+constexpr double DRIFT_SAFE = 1.0 + 6.103515625e-05;   // 1 + 2^-14 >= (1 + PEPS) * fp64 rounding slack
 
 struct Grid {
     int d;
@@ -56,6 +55,9 @@ struct Ctrl {
     unsigned long long last_changed;
     double last_shift;
     unsigned int step_done;         // k_step: blocks finished (the last one advances `iter`)
+    unsigned int ref_sel;           // candidate lists: which reference-centre buffer (cref[ref_sel]) they were built at
+    double budget;                  // ... and the centre drift they tolerate (0: exact for the reference only)
+    unsigned int rebuilds;          // candidate-list rebuilds of this fit (diagnostics)
     unsigned int pad1;
 };
 
@@ -125,8 +127,15 @@ __device__ __forceinline__ double maxdist(const double *blo, const double *bhi, 
 // closer, in the canonical fp32 distance, to r than to c.  The objective
 // (1-e)|x-c|^2 - (1+e)|x-r|^2 is separable and concave per axis, so its box
 // minimum is the sum of per-axis endpoint minima.
+//
+// Drift budget dl > 0 (lists reused while every centre stays within dl of the
+// reference position the list was built at): with |x-c| <= Mc and |x-r| <= Mr
+// over the box, (1-e)(|x-c|-dl)^2 - (1+e)(|x-r|+dl)^2 >= S - 2 dl (1+e)(Mc+Mr)
+// - 2 e dl^2, so S > tau + 2 dl (Mc+Mr) (1+e) + 2 dl^2 keeps c dominated by r
+// for any moved centres c', r' (and forces |x-c| > 2 dl).  mr = Mr.
 template <int D>
-__device__ __forceinline__ bool prunable(const double *blo, const double *bhi, const float4 &c, const float4 &r) {
+__device__ __forceinline__ bool prunable(const double *blo, const double *bhi, const float4 &c, const float4 &r,
+                                         double dl = 0.0, double mr = 0.0) {
     const double em = 1.0 - PEPS, ep = 1.0 + PEPS;
     double s = 0.0;
     for (int a = 0; a < D; ++a) {
@@ -136,7 +145,9 @@ __device__ __forceinline__ bool prunable(const double *blo, const double *bhi, c
         double gh = em * (ch * ch) - ep * (rh * rh);
         s += fmin(gl, gh);
     }
-    return s > PTAU;
+    if (!(dl > 0.0)) return s > PTAU;
+    const double mc = sqrt(maxdist<D>(blo, bhi, c));
+    return s > PTAU + (2.0 * dl * (mc + mr) + 2.0 * dl * dl) * DRIFT_SAFE;
 }
 
 template <typename T> __device__ __forceinline__ float to_f(T v);
@@ -313,6 +324,7 @@ template <int D> constexpr int cand_capc() { return D >= 4 ? 1024 : CAPC; }
 #endif
 constexpr int CAND_TPB = PCM_CAND_TPB;   // threads per candidate block (one child cell per wave at a time)
 constexpr int CAND_KBITS = 4096;         // bitmap capacity (larger K: direct ballot compaction)
+constexpr int STEP_RB = 4;               // k_step: statistics rows per thread with loads in flight together
 
 #ifdef PCM_DBG_TIMING
 __device__ unsigned long long g_dbg_t[8192][8];
@@ -338,7 +350,8 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // C: the K centres, in global memory (k_cand) or in LDS (k_step).
 template <int D>
 __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K, uint32_t *__restrict__ fc_cnt,
-                                          float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab, int BPC) {
+                                          float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab, int BPC,
+                                          double dl = 0.0) {
     constexpr int CAP = cand_capc<D>();
     const long long I = blockIdx.x / BPC;
     const int bsub = blockIdx.x % BPC;
@@ -383,9 +396,10 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         __syncthreads();
         DBG_T(4);
         const float4 r = C[(int)min((unsigned long long)(K - 1), rkey & 0xFFFFFFFFull)];
+        const double mr = dl > 0.0 ? sqrt(maxdist<D>(blo, bhi, r)) : 0.0;
         if (bitmap) {
             for (int j = tid; j < K; j += CAND_TPB)
-                if (!prunable<D>(blo, bhi, C[j], r)) atomicOr(&kbits[j >> 6], 1ull << (j & 63));
+                if (!prunable<D>(blo, bhi, C[j], r, dl, mr)) atomicOr(&kbits[j >> 6], 1ull << (j & 63));
             __syncthreads();
             DBG_T(5);
             if (wv == 0) {
@@ -408,7 +422,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
             uint32_t total = 0;
             for (int base = 0; base < K; base += CAND_TPB) {
                 const int j = base + tid;
-                const bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r);
+                const bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r, dl, mr);
                 const unsigned long long bal = __ballot(keep);
                 if (lane == 0) wcnt[wv] = __popcll(bal);
                 __syncthreads();
@@ -495,6 +509,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                 if (bl >= (int)mp) bl = 0;
             }
             const float4 r = PF ? C[bl] : prec[bl];
+            const double mr = dl > 0.0 ? sqrt(maxdist<D>(blo, bhi, r)) : 0.0;
             uint32_t total = 0;
             for (uint32_t base = 0; base < mp; base += 64) {
                 const uint32_t l = base + lane;
@@ -502,7 +517,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                 const uint32_t lc = in ? l : (uint32_t)bl;
                 const float4 c = PF ? C[lc] : prec[lc];
                 const int j = PF ? (int)lc : pidx[lc];
-                const bool keep = in && !prunable<D>(blo, bhi, c, r);
+                const bool keep = in && !prunable<D>(blo, bhi, c, r, dl, mr);
                 const unsigned long long bal = __ballot(keep);
                 const uint32_t pos = total + __popcll(bal & ((1ull << lane) - 1ull));
                 if (keep && pos < (uint32_t)CAPF) {
@@ -519,13 +534,54 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     DBG_T(2);
 }
 
+// Standalone candidate lists, exact for the current centres C (drift budget 0;
+// fit start, relocation resume, final E-step, K > KSTEP_MAX): the reference
+// buffer cref[ctrl->ref_sel] := C so that k_step measures drift from C.
 template <int D>
 __global__ __launch_bounds__(CAND_TPB) void k_cand(Grid g, const float4 *__restrict__ C, int K,
                                               uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                              int32_t *__restrict__ fc_lab, const Ctrl *__restrict__ ctrl, int gate,
-                                              int bpc) {
+                                              int32_t *__restrict__ fc_lab, Ctrl *__restrict__ ctrl, int gate,
+                                              int bpc, float4 *__restrict__ cref) {
     if (gate && gated(ctrl)) return;
+    float4 *ref = cref + (size_t)ctrl->ref_sel * K;
+    for (long long j = blockIdx.x * (long long)CAND_TPB + threadIdx.x; j < K; j += (long long)gridDim.x * CAND_TPB)
+        ref[j] = C[j];
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->budget = 0.0;
     cand_body<D>(g, C, K, fc_cnt, fc_rec, fc_lab, bpc);
+}
+
+// Candidate records refreshed to the new centres (lists still valid under the
+// drift budget): the children of coarse cell blockIdx.x / BPC handled by this
+// block (the partition of cand_body); CAND_TPB / nch threads per child, every
+// load of a child's count and ids issued in parallel (no per-child loop).
+template <int D>
+__device__ __forceinline__ void refresh_body(const Grid &g, const float4 *cn, const uint32_t *__restrict__ fc_cnt,
+                                             float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
+                                             int BPC) {
+    const long long I = blockIdx.x / BPC;
+    const int bsub = blockIdx.x % BPC;
+    int ci[MAXD];
+    decode(I, g.GC, D, ci);
+    int nchild = 1;
+    for (int a = 0; a < D; ++a) nchild *= 4;
+    const int cpb = (nchild + BPC - 1) / BPC;
+    const int c0 = bsub * cpb, c1 = min(nchild, (bsub + 1) * cpb);
+    const int per = max(1, CAND_TPB / max(1, c1 - c0));     // threads per child
+    for (int ch = c0 + (int)threadIdx.x / per; ch < c1; ch += CAND_TPB / per) {
+        const int sub = (int)threadIdx.x % per;
+        int f[MAXD];
+        bool inside = true;
+#pragma unroll
+        for (int a = D - 1, t = ch; a >= 0; --a, t >>= 2) {
+            f[a] = ci[a] * 4 + (t & 3);
+            inside &= f[a] < g.G[a];
+        }
+        if (!inside) continue;
+        const long long cell = encode(f, g.G, D);
+        const uint32_t m = fc_cnt[cell];
+        if (m == FULL) continue;
+        for (uint32_t p = sub; p < m; p += per) fc_rec[cell * CAPF + p] = cn[fc_lab[cell * CAPF + p]];
+    }
 }
 
 // ------------------------------------------------------------------ assign
@@ -663,7 +719,8 @@ struct LloydArgs {
     const float4 *C;                // all centres (FULL cells)
     int K;
     int q[MAXD];
-    unsigned long long *partials;   // [2][K][D+1]: iteration parity halves
+    unsigned long long *partials;   // accumulation target: + (iter & 1) * pstride
+    long long pstride;              // K*(D+1): single-GPU parity halves; 0: the all-reduce buffer itself
     const Ctrl *ctrl;
 };
 
@@ -898,7 +955,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     LOAD_X(xb, item_off(1));
     __syncthreads();
 
-    unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.K * (D + 1);
+    unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.pstride;
     int par = 0;
 
     auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx) -> bool {
@@ -1004,21 +1061,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         if (!step(xb, xa)) break;
         if (!step(xc, xb)) break;
     }
-}
-
-// stats := partials[parity] (the all-reduce input); partials[parity] := 0; stats[K*(D+1)] = 0
-template <int D>
-__global__ __launch_bounds__(256) void k_fold(unsigned long long *__restrict__ partials, int K,
-                                              unsigned long long *__restrict__ stats, Ctrl *__restrict__ ctrl) {
-    if (gated(ctrl)) return;
-    const int n = K * (D + 1);
-    unsigned long long *src = partials + (size_t)(ctrl->iter & 1u) * n;
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        stats[i] = src[i];
-        src[i] = 0ull;
-    }
-    if (i == n) stats[n] = 0ull;
 }
 
 // Single block of 1024 threads.  Optionally first folds partials[parity] into
@@ -1165,6 +1207,10 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
     }
     ssum[tid] = acc;
     __syncthreads();
+    // statistics read in place (all-reduce buffer / resume): zero them for the
+    // next iteration's accumulation (every read above precedes the barrier)
+    if (!partials)
+        for (int i = tid; i < n + 1; i += 1024) stats[i] = 0ull;
     for (int st = 512; st >= 64; st >>= 1) {
         if (tid < st) ssum[tid] = ssum[tid] + ssum[tid + st];
         __syncthreads();
@@ -1197,66 +1243,119 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
 }
 
 // ------------------------------------------------------------------ fused update + candidates
-// One launch per iteration for the centre update AND the next candidate lists
-// (k_global + k_cand fused; K <= KSTEP_MAX).  Every block recomputes the K new
-// centres from the integer statistics into LDS -- deterministic, so all blocks
-// agree bit for bit -- and builds its candidate lists from them; one extra
-// block (the last) does only the bookkeeping of k_global (statistics-equality test, fixed-tree shift,
-// history, flags, C := new centres) and zeroes the other parity half of the
-// partials.  An empty cluster halts (that block snapshots the statistics; the
-// host relocates, then k_global + k_cand resume).  src: the all-reduced stats
-// (multi-GPU) or nullptr = partials[parity] (single GPU).
+// One launch per iteration for the centre update AND the next iteration's
+// candidate lists (K <= KSTEP_MAX).  Every block recomputes the K new centres
+// from the integer statistics into LDS -- deterministic, so all blocks agree
+// bit for bit -- and then either
+//  * REFRESHES the records of its cells' lists to the new centres, when every
+//    centre is still within the lists' drift budget of the reference position
+//    the lists were built at (see prunable: the lists stay exact), or
+//  * REBUILDS its cells' lists at the new centres with a new budget
+//    alpha * (this iteration's largest centre shift), capped at kappa * the
+//    smallest cell width (above that: budget 0, exact lists).
+// The decision uses maxima over all K centres computed identically in every
+// block.  One extra block (the last) does the bookkeeping of k_global
+// (statistics-equality test, fixed-tree shift, history); the last block to
+// finish publishes C := new centres, the new reference/budget, the iteration
+// and the flags, and (stats_in) zeroes the all-reduce buffer for the next
+// accumulation.  An empty cluster halts (that block snapshots the statistics;
+// the host relocates, then k_global + k_cand resume).  stats_in: the
+// all-reduced statistics (multi-GPU) or nullptr = partials[parity] (single GPU).
+#ifndef PCM_STEP_WAVES
+#define PCM_STEP_WAVES 4   // >= 4 waves/SIMD (VGPR <= 128): 4 resident 256-thread blocks per CU
+#endif
 template <int D>
-__global__ __launch_bounds__(CAND_TPB) void k_step(Grid g, const unsigned long long *__restrict__ stats_in,
+__global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsigned long long *__restrict__ stats_in,
                                               unsigned long long *__restrict__ partials, int K, QExp qe,
                                               unsigned long long *__restrict__ held,
                                               unsigned long long *__restrict__ prev, float4 *__restrict__ C,
+                                              float4 *__restrict__ cref,
                                               unsigned long long *__restrict__ hist_changed,
                                               double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl,
                                               uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                              int32_t *__restrict__ fc_lab, int bpc) {
+                                              int32_t *__restrict__ fc_lab, int bpc, double alpha, double dl_cap) {
     if (gated(ctrl)) return;
     DBG_T(0);
     extern __shared__ __attribute__((aligned(16))) float4 cn[];   // [K]
-    __shared__ unsigned s_empty;
+    __shared__ unsigned s_empty, s_last;
     __shared__ unsigned long long s_neq;
     __shared__ double ssum[1024];
-    const int tid = threadIdx.x, lane = tid & 63;
+    __shared__ double s_dmax[CAND_TPB / 64], s_smax[CAND_TPB / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = K * (D + 1);
     const unsigned par = ctrl->iter & 1u;
+    const unsigned sel = ctrl->ref_sel;
+    const double budget = ctrl->budget;
     const unsigned long long *src = stats_in ? stats_in : partials + (size_t)par * n;
+    const float4 *ref = cref + (size_t)sel * K;
     const bool b0 = blockIdx.x == gridDim.x - 1;   // the bookkeeping block (builds no candidate lists)
     if (tid == 0) { s_empty = 0; s_neq = 0ull; }
     __syncthreads();
     unsigned ne = 0;
     unsigned long long neq = 0;
-    for (int j = tid; j < K; j += CAND_TPB) {
-        unsigned long long row[D + 1];
+    double dmax = 0.0, smax = 0.0;   // squared drift from the reference / squared shift this iteration
+    // rows j = tid + CAND_TPB * (j0 + u): STEP_RB rows' loads are all issued before any is used
+    constexpr int RB = STEP_RB;
+    for (int j0 = 0; j0 * CAND_TPB < K; j0 += RB) {
+        unsigned long long row[RB][D + 1], pv[RB][D + 1];
+        float4 rj[RB], oj[RB];
 #pragma unroll
-        for (int a = 0; a <= D; ++a) row[a] = src[(size_t)j * (D + 1) + a];
-        const unsigned long long c = row[D];
-        float out[4] = {0.f, 0.f, 0.f, 0.f};
-        if (c > 0) {
+        for (int u = 0; u < RB; ++u) {
+            const int j = tid + CAND_TPB * (j0 + u);
+            const int jj = j < K ? j : K - 1;
+#pragma unroll
+            for (int a = 0; a <= D; ++a) row[u][a] = src[(size_t)jj * (D + 1) + a];
+            rj[u] = ref[jj];
+            oj[u] = C[jj];
+            if (b0)
+#pragma unroll
+                for (int a = 0; a <= D; ++a) pv[u][a] = prev[(size_t)jj * (D + 1) + a];
+        }
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            const int j = tid + CAND_TPB * (j0 + u);
+            if (j >= K) break;
+            const unsigned long long c = row[u][D];
+            float out[4] = {0.f, 0.f, 0.f, 0.f};
+            if (c > 0) {
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    const double m = ((double)(long long)row[u][a] * __builtin_ldexp(1.0, -qe.q[a])) / (double)c;
+                    out[a] = (float)m;
+                }
+            } else {
+                ++ne;
+            }
+            const float4 v = make_float4(out[0], out[1], out[2], out[3]);
+            cn[j] = v;
+            double dr = 0.0, ds = 0.0;
 #pragma unroll
             for (int a = 0; a < D; ++a) {
-                const double m = ((double)(long long)row[a] * __builtin_ldexp(1.0, -qe.q[a])) / (double)c;
-                out[a] = (float)m;
+                const double e1 = (double)comp(v, a) - (double)comp(rj[u], a);
+                const double e2 = (double)comp(v, a) - (double)comp(oj[u], a);
+                dr += e1 * e1;
+                ds += e2 * e2;
             }
-        } else {
-            ++ne;
-        }
-        cn[j] = make_float4(out[0], out[1], out[2], out[3]);
-        if (b0) {   // convergence (sklearn: labels equal): raw statistics equal the previous ones
+            dmax = fmax(dmax, dr);
+            smax = fmax(smax, ds);
+            if (b0) {   // convergence (sklearn: labels equal): raw statistics equal the previous ones
 #pragma unroll
-            for (int a = 0; a <= D; ++a) {
-                neq += (row[a] != prev[(size_t)j * (D + 1) + a]) ? 1ull : 0ull;
-                prev[(size_t)j * (D + 1) + a] = row[a];
+                for (int a = 0; a <= D; ++a) {
+                    neq += (row[u][a] != pv[u][a]) ? 1ull : 0ull;
+                    prev[(size_t)j * (D + 1) + a] = row[u][a];
+                }
             }
         }
     }
+    for (int o = 32; o > 0; o >>= 1) {
+        dmax = fmax(dmax, __shfl_xor(dmax, o));
+        smax = fmax(smax, __shfl_xor(smax, o));
+    }
+    if (lane == 0) { s_dmax[wv] = dmax; s_smax[wv] = smax; }
     if (ne) atomicAdd(&s_empty, ne);
     if (neq) atomicAdd(&s_neq, neq);
     __syncthreads();
+    DBG_T(6);
     if (b0 && !stats_in)   // the next iteration accumulates into the other half
         for (int i = tid; i < n; i += CAND_TPB) partials[(size_t)(par ^ 1u) * n + i] = 0ull;
     if (s_empty > 0) {
@@ -1271,6 +1370,13 @@ __global__ __launch_bounds__(CAND_TPB) void k_step(Grid g, const unsigned long l
         }
         return;
     }
+    dmax = s_dmax[0];
+    smax = s_smax[0];
+    for (int w = 1; w < CAND_TPB / 64; ++w) { dmax = fmax(dmax, s_dmax[w]); smax = fmax(smax, s_smax[w]); }
+    const double slack = 1.0 + 9.094947017729282e-13;   // 1 + 2^-40: fp64 rounding of the drift norms
+    const bool rebuild = !(sqrt(dmax) * slack <= budget);
+    double dl_new = alpha * sqrt(smax) * slack;
+    if (!(dl_new <= dl_cap)) dl_new = 0.0;
     if (b0) {
         // shift with the fixed tree of k_global: lane L (0..1023) sums j = L + 1024 r
         // sequentially; thread tid plays lanes tid + CAND_TPB u; then halving 512..1
@@ -1295,7 +1401,10 @@ __global__ __launch_bounds__(CAND_TPB) void k_step(Grid g, const unsigned long l
             for (int L = tid; L < st; L += CAND_TPB) ssum[L] = ssum[L] + ssum[L + st];
             __syncthreads();
         }
-        for (int j = tid; j < K; j += CAND_TPB) C[j] = cn[j];
+        if (rebuild) {
+            float4 *nref = cref + (size_t)(sel ^ 1u) * K;
+            for (int j = tid; j < K; j += CAND_TPB) nref[j] = cn[j];
+        }
         if (tid == 0) {
             const uint32_t it = ctrl->iter;
             if (it < ctrl->max_iter) {
@@ -1305,35 +1414,52 @@ __global__ __launch_bounds__(CAND_TPB) void k_step(Grid g, const unsigned long l
             __hip_atomic_store(&ctrl->last_changed, s_neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ctrl->last_shift, ssum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+    } else if (rebuild) {
+        cand_body<D>(g, cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new);
+    } else {
+        refresh_body<D>(g, cn, fc_cnt, fc_rec, fc_lab, bpc);
     }
     DBG_T(3);
-    if (!b0) cand_body<D>(g, cn, K, fc_cnt, fc_rec, fc_lab, bpc);
-    // Every block has read ctrl->iter (parity) before any block can observe the
-    // final count, so only the last block advances the iteration and flags.
+    // Every block has read ctrl (parity, reference, budget) and C before any
+    // block can observe the final count, so only the last block publishes.
+    // Nothing a block writes is read later in this launch except b0's
+    // last_changed / last_shift (sc1 stores, drained before b0's arrival, read
+    // with sc1 loads by the last arriver: MI355X_MICROARCH.md hand-off row 1),
+    // so the arrival needs no L2 write-back fence.
     __syncthreads();
     if (tid == 0) {
-        __threadfence();
-        const unsigned prior = atomicAdd(&ctrl->step_done, 1u);
-        if (prior == gridDim.x - 1) {
-            __threadfence();
-            const unsigned long long changed =
-                __hip_atomic_load(&ctrl->last_changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const double shift = __hip_atomic_load(&ctrl->last_shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t it = ctrl->iter;
-            ctrl->step_done = 0u;
-            ctrl->resume = 0u;
-            uint32_t done = 0;
-            if (changed == 0ull) done = 1u;
-            else if (shift <= ctrl->tol) done = 2u;
-#if defined(PCM_ABL_NOHALT)
-            done = 0u;
-#endif
-            if (!done && it + 1 >= ctrl->max_iter) done = 3u;
-            ctrl->done = done;
-            ctrl->iter = it + 1;
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prior = __hip_atomic_fetch_add(&ctrl->step_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prior == gridDim.x - 1) ? 1u : 0u;
     }
-    (void)lane;
+    __syncthreads();
+    if (!s_last) return;
+    for (int j = tid; j < K; j += CAND_TPB) C[j] = cn[j];
+    if (stats_in)   // every block has read the all-reduced statistics: zero them for the next accumulation
+        for (int i = tid; i < n + 1; i += CAND_TPB) stats_in[i] = 0ull;
+    if (tid == 0) {
+        const unsigned long long changed =
+            __hip_atomic_load(&ctrl->last_changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double shift = __hip_atomic_load(&ctrl->last_shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t it = ctrl->iter;
+        ctrl->step_done = 0u;
+        ctrl->resume = 0u;
+        if (rebuild) {
+            ctrl->ref_sel = sel ^ 1u;
+            ctrl->budget = dl_new;
+            ctrl->rebuilds += 1u;
+        }
+        uint32_t done = 0;
+        if (changed == 0ull) done = 1u;
+        else if (shift <= ctrl->tol) done = 2u;
+#if defined(PCM_ABL_NOHALT)
+        done = 0u;
+#endif
+        if (!done && it + 1 >= ctrl->max_iter) done = 3u;
+        ctrl->done = done;
+        ctrl->iter = it + 1;
+    }
+    DBG_T(7);
 }
 
 // ------------------------------------------------------------------ relocation

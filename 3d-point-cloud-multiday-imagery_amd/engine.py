@@ -119,7 +119,7 @@ class Engine:
         return dict(halt=st.halt, done=st.done, iter=st.iter, n_empty=st.n_empty, inertia=st.inertia,
                     last_changed=st.last_changed, last_shift=st.last_shift,
                     inertia_limbs=[int(v) for v in st.inertia_limbs], inertia_scale=int(st.inertia_scale),
-                    inertia_overflow=int(st.inertia_overflow))
+                    inertia_overflow=int(st.inertia_overflow), list_rebuilds=int(st.list_rebuilds))
 
     def reloc_candidates(self, m: int) -> torch.Tensor:
         rec = torch.zeros(m * RELOC_RECORD_BYTES, dtype=torch.uint8, device=self.device)

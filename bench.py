@@ -219,6 +219,8 @@ def main():
     if st["iter"] < total_iters or st["halt"]:
         raise SystemExit(f"timed iterations did not all run: {st}")
     cand = eng.candidate_stats()
+    cand["list_rebuilds"] = st.get("list_rebuilds")
+    cand["iterations"] = st["iter"]
     info = eng.layout_info()
     if world > 1:
         t = torch.tensor([dt, tm["assign_ms"]], dtype=torch.float64, device="cuda")

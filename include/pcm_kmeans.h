@@ -68,6 +68,9 @@ typedef struct pcm_status {
     uint64_t inertia_limbs[3];
     int32_t inertia_scale;
     uint32_t inertia_overflow;   /* > 0: a distance exceeded the bound (inertia = +inf) */
+    uint32_t list_rebuilds;      /* candidate-list rebuilds so far in this fit (the other iterations
+                                    only refreshed the lists' centre records) */
+    uint32_t pad_;
 } pcm_status;
 
 typedef struct pcm_engine pcm_engine;
@@ -101,11 +104,12 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
 int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void *stream);
 
 /* One Lloyd iteration split at the all-reduce:
- *   pcm_iter_local   candidate lists + assign/accumulate; folds the local
- *                    integer statistics into the buffer of pcm_stats_ptr;
+ *   pcm_iter_local   assign + exact accumulation of the local integer
+ *                    statistics straight into the buffer of pcm_stats_ptr;
  *   (caller all-reduces that buffer with SUM over ranks when world size > 1)
  *   pcm_iter_global  empty-cluster check (may set halt), averaging, shift,
- *                    convergence flags.
+ *                    convergence flags, the next iteration's candidate lists;
+ *                    zeroes the statistics buffer for the next iteration.
  * Both are gated on the device: after convergence or halt they are no-ops. */
 int pcm_iter_local(pcm_engine *e, void *stream);
 int pcm_iter_global(pcm_engine *e, void *stream);

@@ -102,7 +102,7 @@ class OracleEngine:
 
     def status(self):
         return dict(halt=self.halt, done=self.done, iter=self.it, n_empty=self.n_empty, inertia=self.inertia,
-                    inertia_limbs=list(self.limbs), inertia_scale=R.inertia_scale(self.q), inertia_overflow=0,
+                    inertia_limbs=list(self.limbs), inertia_scale=R.inertia_scale(self.q), inertia_overflow=0, list_rebuilds=0,
                     last_changed=self.hist_changed[-1] if self.hist_changed else 0,
                     last_shift=self.hist_shift[-1] if self.hist_shift else 0.0)
 

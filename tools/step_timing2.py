@@ -1,0 +1,39 @@
+"""Calibration (debug build -DPCM_DBG_TIMING): per-block phase times of the
+fused k_step of the last of `iters` iterations (config 3).  usage:
+python tools/step_timing2.py SO_PATH [iters]"""
+import ctypes, os, sys
+import numpy as np
+os.environ["PCM_SO"] = sys.argv[1]
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pcm_amd import lloyd, _lib
+from pcm_amd.engine import Engine, synth_rows, synth_uniform
+N, K, D = 100_000_000, 1024, 3
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+X = synth_uniform(N, D, seed=0, start=0)
+C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0)
+eng = Engine(D, K, torch.float32, max_iter=50)
+lloyd.prepare(eng, X, None)
+eng.begin(C0, 0.0, 50)
+eng.iterate(iters); torch.cuda.synchronize()
+st = eng.status()
+lib = _lib.load()
+lib.pcm_debug_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+nb = 8192
+buf = np.zeros((nb, 8), np.uint64)
+assert lib.pcm_debug_timing(buf.ctypes.data_as(ctypes.c_void_p), nb) == 0
+t = buf.astype(np.int64)
+nbk = int((t[:, 0] > 0).sum())
+t = t[:nbk]
+t0 = t[:, 0].min()
+us = lambda v: v / 100.0   # s_memrealtime: 100 MHz
+print(f"iters {st['iter']} rebuilds {st['list_rebuilds']} blocks {nbk}")
+print("block start spread us: p50 %.1f p90 %.1f max %.1f" % tuple(us(np.percentile(t[:, 0] - t0, q)) for q in (50, 90, 100)))
+w = t[:-1]
+print("centres+drift us (start->6): p50 %.1f max %.1f" % (us(np.median(w[:, 6] - w[:, 0])), us((w[:, 6] - w[:, 0]).max())))
+print("body us (6->3): p50 %.1f max %.1f" % (us(np.median(w[:, 3] - w[:, 6])), us((w[:, 3] - w[:, 6]).max())))
+b = t[-1]
+print("b0: centres %.1f, bookkeeping %.1f us" % (us(b[6] - b[0]), us(b[3] - b[6])))
+print("end of bodies (rel. first start) us: p50 %.1f max %.1f" % (us(np.median(t[:, 3] - t0)), us(t[:, 3].max() - t0)))
+last = t[:, 7].max()
+print("last block finished at %.1f us" % us(last - t0))
