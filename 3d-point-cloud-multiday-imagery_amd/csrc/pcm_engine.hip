@@ -465,8 +465,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
-        k_gather<TT, D><<<blocks_for((e->npad + GATHER_PER - 1) / GATHER_PER), 256, 0, s>>>((const TT *)X, n, e->npad,
-                                                                                          e->perm, (TT *)e->xs);
+        k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs);
         LAUNCHCHK();
         return 0;
     });
@@ -923,7 +922,8 @@ int pcm_synth_uniform(float *out, int64_t n, int d, uint64_t seed, int64_t start
     return 0;
 }
 
-// Debug (not in the public header): copy the sorted layout to device buffers.
+// Debug (not in the public header): copy the sorted layout to device buffers
+// (xs in the AoSoA-4 order of pcm_kernels.hpp xs_index).
 int pcm_debug_layout(pcm_engine *e, void *xs_out, int32_t *lab_out, uint32_t *perm_out, void *stream) {
     if (!e || !e->layout_ready) return fail(PCM_E_STATE, "layout not built");
     hipStream_t s = (hipStream_t)stream;

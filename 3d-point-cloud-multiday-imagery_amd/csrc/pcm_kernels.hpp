@@ -235,28 +235,27 @@ __global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long lo
     vals[i] = (uint32_t)i;
 }
 
-// AoS gather into cell order: GATHER_PER consecutive destination rows per
-// thread (their perm entries loaded at once), so every thread keeps
-// GATHER_PER * D independent random reads in flight.
-constexpr int GATHER_PER = 1;   // 4 measured slower (3.06 vs 2.5 ms at 100M): random 12-B rows are HBM-line bound
+// Sorted point layout "AoSoA-4": the points in cell order, in groups of 4
+// consecutive points stored coordinate-major -- [x0 x1 x2 x3][y0 .. y3][z0 .. z3]
+// -- so one lane's 4 points arrive from b128 loads already paired for the
+// packed (v_pk_*) distance arithmetic, with no register shuffling.
+template <int D>
+__device__ __forceinline__ long long xs_index(long long i, int a) {
+    return ((i >> 2) * D + a) * 4 + (i & 3);
+}
+
+// Gather into cell order (AoSoA-4).  Random 12-B row reads are HBM-line
+// bound; one destination row per thread measured fastest (4 per thread: 3.06
+// vs 2.5 ms at 100M).
+constexpr int GATHER_PER = 1;
 template <typename T, int D>
 __global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long long n, long long npad,
                                                 const uint32_t *__restrict__ perm, T *__restrict__ xs) {
-    const long long i0 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * GATHER_PER;
-    if (i0 >= npad) return;
-    long long src[GATHER_PER];
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= npad) return;
+    const long long src = i < n ? (long long)perm[i] : -1;
 #pragma unroll
-    for (int e = 0; e < GATHER_PER; ++e) src[e] = (i0 + e < n) ? (long long)perm[i0 + e] : -1;
-    T v[GATHER_PER][D];
-#pragma unroll
-    for (int e = 0; e < GATHER_PER; ++e)
-#pragma unroll
-        for (int a = 0; a < D; ++a) v[e][a] = src[e] >= 0 ? X[src[e] * D + a] : (T)0.0f;
-#pragma unroll
-    for (int e = 0; e < GATHER_PER; ++e)
-        if (i0 + e < npad)
-#pragma unroll
-            for (int a = 0; a < D; ++a) xs[(i0 + e) * D + a] = v[e][a];
+    for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = src >= 0 ? X[src * D + a] : (T)0.0f;
 }
 
 // cell_start[c] = first sorted index with key >= c, for c in [0, ncells]
@@ -653,16 +652,17 @@ __device__ __forceinline__ void load_x(Raw<T, D> &r, rsrc_t rs, unsigned off_pt)
     }
 }
 #define LOAD_X(dst, off) load_x<T, D>(dst, rx, off)
+// AoSoA-4 (xs_index): word a*4 + e holds coordinate a of the lane's point e
 template <int D>
 __device__ __forceinline__ void unpack_x(const Raw<float, D> &r, float (&x)[4][D]) {
     for (int e = 0; e < 4; ++e)
-        for (int a = 0; a < D; ++a) x[e][a] = __uint_as_float(r.w[e * D + a]);
+        for (int a = 0; a < D; ++a) x[e][a] = __uint_as_float(r.w[a * 4 + e]);
 }
 template <int D>
 __device__ __forceinline__ void unpack_x(const Raw<__half, D> &r, float (&x)[4][D]) {
     for (int e = 0; e < 4; ++e)
         for (int a = 0; a < D; ++a) {
-            const int k = e * D + a;
+            const int k = a * 4 + e;
             const unsigned word = r.w[k >> 1];
             const unsigned short hb = (unsigned short)((k & 1) ? (word >> 16) : (word & 0xffffu));
             x[e][a] = __half2float(__ushort_as_half(hb));
@@ -1358,7 +1358,11 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
     DBG_T(6);
     if (b0 && !stats_in)   // the next iteration accumulates into the other half
         for (int i = tid; i < n; i += CAND_TPB) partials[(size_t)(par ^ 1u) * n + i] = 0ull;
+#if defined(PCM_ABL_NOHALT)
+    if (false) {   // ablation build: never halt (statistics are meaningless)
+#else
     if (s_empty > 0) {
+#endif
         if (b0) {
             for (int i = tid; i < n; i += CAND_TPB) held[i] = src[i];
             if (tid == 0) {
@@ -1472,7 +1476,7 @@ __global__ __launch_bounds__(256) void k_reloc_keys(const T *__restrict__ xs, lo
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= n) return;
     float x[D];
-    for (int a = 0; a < D; ++a) x[a] = to_f<T>(xs[i * D + a]);
+    for (int a = 0; a < D; ++a) x[a] = to_f<T>(xs[xs_index<D>(i, a)]);
     float d = dist_canon<D>(x, C[(int)lab[i]]);
     unsigned long long g = (unsigned long long)(gidx0 + perm[i]);
     keys[i] = ((unsigned long long)__float_as_uint(d) << 32) | (0xffffffffull - (g & 0xffffffffull));
@@ -1500,7 +1504,7 @@ __global__ void k_reloc_gather(const unsigned long long *__restrict__ keys, cons
         r.key = keys[t];
         r.label = (int)lab[i];
         r.valid = 1;
-        for (int a = 0; a < D; ++a) r.xq[a] = fixed_i(to_f<T>(xs[i * D + a]), qe.q[a]);
+        for (int a = 0; a < D; ++a) r.xq[a] = fixed_i(to_f<T>(xs[xs_index<D>(i, a)]), qe.q[a]);
     }
     out[t] = r;
 }

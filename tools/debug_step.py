@@ -40,7 +40,7 @@ def check(X, C, label):
                                ctypes.c_void_p(pm.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
     npad = ((n + 3) // 4) * 4 + 4
-    xs = xs.cpu().numpy().reshape(npad, d)[:n]
+    xs = xs.cpu().numpy().reshape(npad // 4, d, 4).transpose(0, 2, 1).reshape(npad, d)[:n]   # AoSoA-4
     ls = ls.cpu().numpy()
     pm = pm.cpu().numpy().astype(np.int64)
     print("  debug rc", rc_, "perm is permutation:", np.array_equal(np.sort(pm), np.arange(n)),
