@@ -14,9 +14,10 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 SO_PATH = os.environ.get("PCM_SO") or os.path.join(PKG_DIR, "libpcmkm.so")
-SOURCES = [os.path.join(PKG_DIR, "csrc", "pcm_engine.hip"), os.path.join(PKG_DIR, "csrc", "pcm_kernels.hpp"),
-           os.path.join(PKG_DIR, "csrc", "pcm_kpp.hpp"), os.path.join(PKG_DIR, "csrc", "pcm_cloud.hpp"),
-           os.path.join(REPO_DIR, "include", "pcm_kmeans.h")]
+UNITS = [os.path.join(PKG_DIR, "csrc", "pcm_engine.hip"), os.path.join(PKG_DIR, "csrc", "pcm_dense.hip")]
+SOURCES = UNITS + [os.path.join(PKG_DIR, "csrc", h) for h in ("pcm_kernels.hpp", "pcm_kpp.hpp", "pcm_cloud.hpp",
+                                                              "pcm_common.hpp")] + \
+    [os.path.join(REPO_DIR, "include", "pcm_kmeans.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
 
@@ -27,7 +28,9 @@ EXPORTS = [
     "pcm_bind_stats", "pcm_reloc_candidates", "pcm_reloc_apply", "pcm_final", "pcm_labels", "pcm_get_centers",
     "pcm_history", "pcm_read_status", "pcm_layout_info", "pcm_candidate_stats", "pcm_synth_uniform",
     "pcm_assign_bruteforce", "pcm_timing", "pcm_timing_read", "pcm_synth_rows", "pcm_kmeanspp", "pcm_cloud_assemble",
-    "pcm_inertia_value",
+    "pcm_inertia_value", "pcm_kmeanspp_workspace",
+    "pcm_dense_create", "pcm_dense_destroy", "pcm_dense_begin", "pcm_dense_iterate", "pcm_dense_final",
+    "pcm_dense_status", "pcm_dense_outputs", "pcm_dense_kmeanspp_workspace", "pcm_dense_kmeanspp",
 ]
 ABI_VERSION = 2
 
@@ -58,7 +61,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     """Compile ``libpcmkm.so`` for gfx950 with hipcc (works without a GPU)."""
     if not force and not needs_build():
         return SO_PATH
-    cmd = [HIPCC, *HIP_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-o", SO_PATH + ".tmp", SOURCES[0]]
+    cmd = [HIPCC, *HIP_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-o", SO_PATH + ".tmp", *UNITS]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -95,9 +98,19 @@ def _declare(lib):
         "pcm_timing": ([P, I], I),
         "pcm_timing_read": ([P, P, ctypes.POINTER(I)], I),
         "pcm_synth_rows": ([P, P, I64, I, ctypes.c_uint64, P], I),
-        "pcm_kmeanspp": ([P, I64, I, I, I, I64, P, I, P, P], I),
+        "pcm_kmeanspp": ([P, I64, I, I, I, I64, P, P, P, ctypes.c_size_t, P], I),
+        "pcm_kmeanspp_workspace": ([I64, I, I, I, ctypes.POINTER(ctypes.c_size_t)], I),
         "pcm_cloud_assemble": ([P, P, I64, I64, D, P, P, ctypes.POINTER(I64), P, P], I),
         "pcm_inertia_value": ([P, I, ctypes.c_uint32], D),
+        "pcm_dense_create": ([I, I64, I, I, I, I, ctypes.POINTER(P)], I),
+        "pcm_dense_destroy": ([P], I),
+        "pcm_dense_begin": ([P, P, P, P, D, I, P], I),
+        "pcm_dense_iterate": ([P, I, P], I),
+        "pcm_dense_final": ([P, P], I),
+        "pcm_dense_status": ([P, ctypes.POINTER(PcmStatus), P], I),
+        "pcm_dense_outputs": ([P, P, P, P, P, I, P], I),
+        "pcm_dense_kmeanspp_workspace": ([I64, I, I, I, I, ctypes.POINTER(ctypes.c_size_t)], I),
+        "pcm_dense_kmeanspp": ([P, I64, I, I, I, I, I64, P, I, P, P, ctypes.c_size_t, P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -17,6 +17,7 @@
 #include "pcm_kernels.hpp"
 #include "pcm_kpp.hpp"
 #include "pcm_cloud.hpp"
+#include "pcm_common.hpp"
 #include "pcm_kmeans.h"
 
 using namespace pcm;
@@ -29,6 +30,8 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 }  // namespace
+
+int pcm_fail(int code, const std::string &msg) { return fail(code, msg); }
 
 #define HIPCHK(expr)                                                                             \
     do {                                                                                         \
@@ -176,17 +179,12 @@ hipError_t ensure(P *&p, size_t &cap, size_t need) {
 
 size_t align_up(size_t v, size_t a = 256) { return (v + a - 1) / a * a; }
 
-// Choose the pruning grid: about min(32 K, n / 2800) roughly cubic cells over
-// the bounding box (degenerate axes get one cell).
-void choose_grid(pcm_engine *e) {
-    Grid &g = e->g;
+// Roughly cubic grid of about `target` cells over the box [lo, hi]
+// (degenerate axes get one cell); F = 4 fine cells per coarse cell per axis.
+void make_grid(Grid &g, int d, const double *lo, const double *hi, double target) {
     g = Grid{};
-    g.d = e->d;
+    g.d = d;
     g.F = 4;   // fixed: k_cand assumes 4 fine cells per coarse cell per axis
-    // ~2.8k points per cell: fewer, fuller tiles (a tile round is 1024 points)
-    // outweigh the slightly longer candidate lists (swept on 12.5M / 100M clouds)
-    double target = std::min(32.0 * e->k, (double)e->n / 2800.0);
-    if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     target = std::max(1.0, std::min(target, (double)(1 << 18)));
     double vol = 1.0;
     int nondeg = 0;
@@ -195,10 +193,10 @@ void choose_grid(pcm_engine *e) {
         g.G[a] = 1;
         g.GC[a] = 1;
     }
-    for (int a = 0; a < e->d; ++a) {
-        double ex = e->hi[a] - e->lo[a];
+    for (int a = 0; a < d; ++a) {
+        double ex = hi[a] - lo[a];
         g.ext[a] = ex;
-        g.lo[a] = e->lo[a];
+        g.lo[a] = lo[a];
         maxext = std::max(maxext, ex);
         if (ex > 0) {
             vol *= ex;
@@ -206,26 +204,26 @@ void choose_grid(pcm_engine *e) {
         }
     }
     if (nondeg > 0) {
-        double s = std::pow(vol / target, 1.0 / nondeg);
-        for (int a = 0; a < e->d; ++a) {
+        double sz = std::pow(vol / target, 1.0 / nondeg);
+        for (int a = 0; a < d; ++a) {
             if (g.ext[a] > 0) {
-                long long G = std::llround(g.ext[a] / s);
+                long long G = std::llround(g.ext[a] / sz);
                 g.G[a] = (int)std::max(1LL, std::min(G, 4096LL));
             }
         }
     }
     long long nc = 1;
-    for (int a = 0; a < e->d; ++a) nc *= g.G[a];
+    for (int a = 0; a < d; ++a) nc *= g.G[a];
     while (nc > (1LL << 20)) {   // keep keys and candidate tables bounded
         int amax = 0;
-        for (int a = 1; a < e->d; ++a)
+        for (int a = 1; a < d; ++a)
             if (g.G[a] > g.G[amax]) amax = a;
         g.G[amax] = std::max(1, g.G[amax] / 2);
         nc = 1;
-        for (int a = 0; a < e->d; ++a) nc *= g.G[a];
+        for (int a = 0; a < d; ++a) nc *= g.G[a];
     }
     long long ncc = 1;
-    for (int a = 0; a < e->d; ++a) {
+    for (int a = 0; a < d; ++a) {
         g.w[a] = g.ext[a] / g.G[a];
         g.inv[a] = g.ext[a] > 0 ? (double)g.G[a] / g.ext[a] : 0.0;
         g.mg[a] = 1e-7 * g.ext[a];
@@ -235,7 +233,17 @@ void choose_grid(pcm_engine *e) {
     g.ncells = nc;
     g.ncoarse = ncc;
     // fp32 distances overflow beyond ~1.8e19: no pruning then (brute force is exact)
-    g.prune = (maxext < 1e18 && e->k > 1) ? 1 : 0;
+    g.prune = (maxext < 1e18) ? 1 : 0;
+}
+
+// The Lloyd engine's pruning grid: about min(32 K, n / 2800) cells -- ~2.8k
+// points per cell: fewer, fuller tiles (a tile round is 1024 points) outweigh
+// the slightly longer candidate lists (swept on 12.5M / 100M clouds).
+void choose_grid(pcm_engine *e) {
+    double target = std::min(32.0 * e->k, (double)e->n / 2800.0);
+    if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
+    make_grid(e->g, e->d, e->lo, e->hi, target);
+    if (e->k <= 1) e->g.prune = 0;
 }
 
 int blocks_for(long long n, int bs = 256) { return (int)std::max(1LL, (n + bs - 1) / bs); }
@@ -963,59 +971,161 @@ int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int 
     });
 }
 
-// k-means++ seeding (oracle/kpp_ref.py; sklearn/cluster/_kmeans.py:174-272).
+// k-means++ seeding (oracle/kpp_ref.py; sklearn/cluster/_kmeans.py:174-272):
+// cell layout of X, then 3 launches per centre (csrc/pcm_kpp.hpp).  All
+// device memory comes from the caller's workspace (pcm_kmeanspp_workspace).
+namespace {
+struct KppWs {   // byte offsets into the workspace
+    size_t bbox_part, bbox_out, nonfinite, keys, keys2, vals, perm, inv, xs, closest, cell_start, cmax, bsum, ctl,
+        um, tmp, total;
+    long long nc_max;
+    size_t sort_bytes;
+};
+
+long long kpp_cells_max(long long n, int d) {
+    const double target = std::max(1.0, (double)n / KPP_CELL_PTS);
+    return std::min<long long>(1LL << 20, (long long)std::ceil(std::pow(1.5, d) * target) + 2);
+}
+
+int kpp_layout(long long n, int d, int k, int L, KppWs &w) {
+    const long long npad = ((n + 3) / 4) * 4 + 4;
+    const long long nb = (n + KPP_OB - 1) / KPP_OB;
+    w.nc_max = kpp_cells_max(n, d);
+    w.sort_bytes = 0;
+    if (rocprim::radix_sort_pairs(nullptr, w.sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (uint32_t *)nullptr, (size_t)n, 0u, 21u, (hipStream_t)0) != hipSuccess)
+        return fail(PCM_E_HIP, "kmeanspp sort size query");
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t at = o; o = align_up(o + std::max<size_t>(bytes, 8)); return at; };
+    w.bbox_part = take((size_t)BBOX_BLOCKS * 2 * MAXD * sizeof(float));
+    w.bbox_out = take(2 * MAXD * sizeof(double));
+    w.nonfinite = take(sizeof(unsigned));
+    w.keys = take(n * 4);
+    w.keys2 = take(n * 4);
+    w.vals = take(n * 4);
+    w.perm = take(n * 4);
+    w.inv = take(n * 4);
+    w.xs = take((size_t)npad * d * sizeof(float));
+    w.closest = take(n * 4);
+    w.cell_start = take((w.nc_max + 1) * 4);
+    w.cmax = take(w.nc_max * 4);
+    w.bsum = take(nb * 8);
+    w.ctl = take(sizeof(KppCtl));
+    w.um = take((size_t)std::max(1, (k - 1) * L) * 8);
+    w.tmp = take(w.sort_bytes);
+    w.total = o;
+    return 0;
+}
+
+// oracle/kpp_ref.py kpp_scale: n * 2^s * maxd * (1 + 2^-20) < 2^62
+int kpp_scale(long long n, double maxd) {
+    if (!(maxd > 0.0) || n <= 0) return 0;
+    int e = 0;
+    (void)std::frexp(maxd * (1.0 + std::ldexp(1.0, -20)), &e);
+    int nb = 0;
+    for (unsigned long long v = (unsigned long long)(n - 1); v; v >>= 1) ++nb;
+    return 62 - std::max(1, nb) - e;
+}
+}  // namespace
+
+int pcm_kmeanspp_workspace(int64_t n, int d, int k, int n_local_trials, size_t *bytes) {
+    if (!bytes || n < 1 || d < 1 || d > MAXD || k < 1 || n_local_trials < 1) return fail(PCM_E_ARG, "bad argument");
+    KppWs w;
+    if (int rc = kpp_layout(n, d, k, n_local_trials, w)) return rc;
+    *bytes = w.total;
+    return 0;
+}
+
 int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, int64_t first_index,
-                 const uint64_t *umant, int scale, int64_t *indices, void *stream) {
+                 const uint64_t *umant, int64_t *indices, void *workspace, size_t workspace_bytes, void *stream) {
     if (!X || !indices || n < 1 || k < 1 || k > n || d < 1 || d > MAXD) return fail(PCM_E_ARG, "bad argument");
     if (n_local_trials < 1 || n_local_trials > KPP_LMAX) return fail(PCM_E_ARG, "n_local_trials must be 1..16");
     if (first_index < 0 || first_index >= n) return fail(PCM_E_ARG, "first_index out of range");
     if (k > 1 && !umant) return fail(PCM_E_ARG, "umant is null");
-    hipStream_t s = (hipStream_t)stream;
-    const long long nblk = (n + KPP_BS - 1) / KPP_BS;
+    if (n >= (1LL << 32) - 8) return fail(PCM_E_ARG, "n must be < 2^32");
     const int L = n_local_trials;
-    float *closest = nullptr;
-    unsigned long long *bsum = nullptr, *um = nullptr;
-    KppState *st = nullptr;
-    int rc = 0;
-    do {
-        hipError_t err;
-        if ((err = hipMalloc(&closest, (size_t)n * sizeof(float))) ||
-            (err = hipMalloc(&bsum, (size_t)nblk * KPP_LMAX * sizeof(unsigned long long))) ||
-            (err = hipMalloc(&st, sizeof(KppState))) ||
-            (err = hipMalloc(&um, (size_t)std::max(1, (k - 1) * L) * sizeof(unsigned long long)))) {
-            rc = fail(PCM_E_NOMEM, std::string("kmeanspp workspace: ") + hipGetErrorString(err));
-            break;
-        }
-        if (k > 1 && (err = hipMemcpyAsync(um, umant, (size_t)(k - 1) * L * sizeof(unsigned long long),
-                                           hipMemcpyHostToDevice, s))) {
-            rc = fail(PCM_E_HIP, "kmeanspp uniforms upload");
-            break;
-        }
-        rc = dispatch_d(d, [&](auto DD) -> int {
-            constexpr int D = decltype(DD)::value;
-            k_kpp_init<D><<<1, 64, 0, s>>>(X, first_index, st);
+    KppWs w;
+    if (int rc = kpp_layout(n, d, k, L, w)) return rc;
+    if (!workspace || workspace_bytes < w.total) return fail(PCM_E_ARG, "workspace too small (pcm_kmeanspp_workspace)");
+    hipStream_t s = (hipStream_t)stream;
+    char *wb = (char *)workspace;
+    float *bbox_part = (float *)(wb + w.bbox_part), *xs = (float *)(wb + w.xs), *closest = (float *)(wb + w.closest),
+          *cmax = (float *)(wb + w.cmax);
+    double *bbox_out = (double *)(wb + w.bbox_out);
+    unsigned *nonfinite = (unsigned *)(wb + w.nonfinite);
+    uint32_t *keys = (uint32_t *)(wb + w.keys), *keys2 = (uint32_t *)(wb + w.keys2), *vals = (uint32_t *)(wb + w.vals),
+             *perm = (uint32_t *)(wb + w.perm), *inv = (uint32_t *)(wb + w.inv),
+             *cell_start = (uint32_t *)(wb + w.cell_start);
+    unsigned long long *bsum = (unsigned long long *)(wb + w.bsum), *um = (unsigned long long *)(wb + w.um);
+    KppCtl *ctl = (KppCtl *)(wb + w.ctl);
+    void *tmp = wb + w.tmp;
+    const long long npad = ((n + 3) / 4) * 4 + 4;
+    const long long nb = (n + KPP_OB - 1) / KPP_OB;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+        ncu = 256;
+    // bounding box (+ non-finite check) -> pruning grid of ~n / KPP_CELL_PTS cells, weight scale
+    const int nblk = (int)std::min<long long>(BBOX_BLOCKS, (n + 255) / 256);
+    HIPCHK(hipMemsetAsync(nonfinite, 0, sizeof(unsigned), s));
+    int rc = dispatch_d(d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_bbox_partial<float, D><<<nblk, 256, 0, s>>>(X, n, bbox_part, nonfinite);
+        LAUNCHCHK();
+        k_bbox_final<D><<<1, 256, 0, s>>>(bbox_part, nblk, bbox_out);
+        LAUNCHCHK();
+        return 0;
+    });
+    if (rc) return rc;
+    double hb[2 * MAXD];
+    unsigned nf = 0;
+    HIPCHK(hipMemcpyAsync(hb, bbox_out, 2 * d * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nf, nonfinite, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (nf) return fail(PCM_E_NONFINITE, "input points contain NaN or Inf");
+    double maxd = 0.0;
+    for (int a = 0; a < d; ++a) maxd += (hb[d + a] - hb[a]) * (hb[d + a] - hb[a]);
+    const int scale = kpp_scale(n, maxd);
+    Grid g;
+    make_grid(g, d, hb, hb + d, std::max(1.0, (double)n / KPP_CELL_PTS));
+    const long long nc = g.ncells;
+    if (nc > w.nc_max) return fail(PCM_E_STATE, "kmeanspp: grid exceeds the workspace bound");
+    unsigned bits = 1;
+    while ((1LL << bits) < nc) ++bits;
+    if (k > 1) HIPCHK(hipMemcpy(um, umant, (size_t)(k - 1) * L * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemsetAsync(bsum, 0, nb * 8, s));
+    HIPCHK(hipMemsetAsync(ctl, 0, sizeof(KppCtl), s));
+    return dispatch_d(d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        // cell layout (the Lloyd engine's kernels): cell ids, radix sort, AoSoA-4 gather, cell starts
+        k_cellid<float, D><<<blocks_for(n), 256, 0, s>>>(X, n, g, keys, vals);
+        LAUNCHCHK();
+        size_t tb = w.sort_bytes;
+        if (hipError_t e2 = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, perm, (size_t)n, 0u, bits, s))
+            return fail(PCM_E_HIP, std::string("kmeanspp sort: ") + hipGetErrorString(e2));
+        k_gather<float, D><<<blocks_for(npad), 256, 0, s>>>(X, n, npad, perm, xs);
+        LAUNCHCHK();
+        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, cell_start);
+        LAUNCHCHK();
+        k_inverse_perm<<<blocks_for(n), 256, 0, s>>>(perm, n, inv);
+        LAUNCHCHK();
+        const int pgrid = ncu * 8;
+        k_kpp_init<D><<<pgrid, 256, 0, s>>>(xs, perm, cell_start, nc, X, first_index, scale, closest, cmax, bsum, ctl,
+                                            (long long *)indices);
+        LAUNCHCHK();
+        for (int c = 1; c < k; ++c) {
+            k_kpp_search<D><<<L + KPP_RED_BLOCKS, KPP_STPB, 0, s>>>(bsum, nb, closest, inv, X, n,
+                                                                    um + (size_t)(c - 1) * L, L, scale, c, cmax, nc,
+                                                                    ctl);
             LAUNCHCHK();
-            for (int c = 0; c < k; ++c) {
-                k_kpp_pass<D><<<(int)nblk, 256, 0, s>>>(X, n, closest, st, scale, bsum);
-                LAUNCHCHK();
-                const bool more = c + 1 < k;
-                k_kpp_select<<<1, 1024, 0, s>>>(bsum, nblk, st, (long long *)indices, c,
-                                                more ? um + (size_t)c * L : nullptr, L);
-                LAUNCHCHK();
-                if (more) {
-                    k_kpp_locate<D><<<L, 1024, 0, s>>>(X, n, closest, st, scale);
-                    LAUNCHCHK();
-                }
-            }
-            return 0;
-        });
-        if (rc) break;
-        if ((err = hipStreamSynchronize(s))) rc = fail(PCM_E_HIP, std::string("kmeanspp: ") + hipGetErrorString(err));
-    } while (0);
-    void *ps[] = {closest, bsum, st, um};
-    for (void *p : ps)
-        if (p) (void)hipFree(p);
-    return rc;
+            k_kpp_eval<D><<<pgrid, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
+            LAUNCHCHK();
+            k_kpp_apply<D><<<pgrid, 256, 0, s>>>(xs, perm, cell_start, g, closest, cmax, bsum, L, scale, c,
+                                                 c + 1 < k ? 1 : 0, (long long *)indices, ctl);
+            LAUNCHCHK();
+        }
+        return 0;
+    });
 }
 
 #ifdef PCM_DBG_TIMING

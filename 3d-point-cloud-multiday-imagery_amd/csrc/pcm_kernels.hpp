@@ -24,8 +24,11 @@ constexpr int MAXD = 4;
 constexpr int CAPC = 256;          // coarse candidate capacity
 constexpr int CAPF = 64;           // fine candidate capacity
 constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-centre ranks)
-constexpr int TPB = 256;           // assign block size
-constexpr int TILE = 8192;         // max points per tile (<= 63 per lane per flush)
+#ifndef PCM_TPB
+#define PCM_TPB 128   // 128 measured 9% faster than 256 at 100M (two-wave barriers), 10% at 12.5M
+#endif
+constexpr int TPB = PCM_TPB;       // assign block size
+constexpr int TILE = 32 * TPB;     // max points per tile: <= 32 per lane, 64 per shared LDS word (see AccL)
 constexpr int KSTEP_MAX = 4096;    // k_step keeps the K new centres in LDS (<= 64 KB of gfx950's 160 KB)
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int QBITS = 25;
@@ -274,6 +277,13 @@ __global__ __launch_bounds__(256) void k_tile_counts(const uint32_t *__restrict_
     if (c >= ncells) return;
     uint32_t n = start[c + 1] - start[c];
     cnt[c] = (n + TILE - 1) / TILE;
+}
+
+// inv[perm[i]] = i (original row -> sorted position)
+__global__ __launch_bounds__(256) void k_inverse_perm(const uint32_t *__restrict__ perm, long long n,
+                                                      uint32_t *__restrict__ inv) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) inv[perm[i]] = (uint32_t)i;
 }
 
 // tile_off[nc] and the tile count (the scan is exclusive: add the last cell's count)
@@ -697,12 +707,12 @@ __device__ __forceinline__ void store_l4(rsrc_t rs, unsigned off, const int (&l)
 #endif
 constexpr int LSLOT = PCM_LSLOT;
 
-// Lane-minor accumulator words shared by threads tid and tid + 128 (different
+// Lane-minor accumulator words shared by threads tid and tid + AW = TPB / 2 (different
 // waves, so an instruction never hits one word twice): word (slot, a) of column
 // c = tid & 127 at (slot*(D+1)+a)*128 + c -- a wave's ds_add_u32 hits 32 distinct
 // banks per half-wave whatever the slots.  A word sums <= 2 x 32 points of
 // |xq| < 2^25 per tile: < 2^31, exact in int32.
-constexpr int AW = 128;
+constexpr int AW = TPB >= 128 ? TPB / 2 : TPB;   // one wave per block: no sharing (same-instruction lanes must not collide)
 template <int D> struct AccL {
     static constexpr int rows = (LSLOT + 1) * (D + 1);   // + junk slot
     static constexpr int words = AW * rows;

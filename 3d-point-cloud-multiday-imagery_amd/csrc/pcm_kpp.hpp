@@ -1,237 +1,404 @@
-// pcm_kpp.hpp — k-means++ seeding on gfx950.
+// pcm_kpp.hpp — k-means++ seeding on gfx950 with exact
+// cell-grid skipping.
 //
 // Restates scikit-learn's _kmeans_plusplus (sklearn/cluster/_kmeans.py:174-272,
 // the KMeans default init, :1012-1019) with the canonical arithmetic of
 // oracle/kpp_ref.py: float32 direct-form distances, integer point weights
-// w = trunc(ldexp(double(d), s)), exact integer potentials and cumulative sums,
-// targets floor(u * pot) computed exactly from u's 53-bit mantissa.
+// w = trunc(ldexp(double(d), s)), exact integer potentials and cumulative sums
+// (in the caller's row order), targets floor(u * pot) computed exactly from u's
+// 53-bit mantissa.
 //
-// Per centre (one step), three stream-ordered launches:
-//   k_kpp_pass    one pass over X: closest := min(closest, d(x, previous best));
-//                 per block, for each of the L candidates, the sum of the
-//                 weights of min(closest, d(x, cand)) -> bsum[block][l]
-//   k_kpp_select  one block: potentials, first argmin (the new centre); for the
-//                 next step's L targets, the block whose prefix crosses each
-//   k_kpp_locate  one block per target: exact index inside its block (scan)
+// The cloud is laid out in pruning-grid cell order (the Lloyd engine's
+// k_cellid / radix sort / AoSoA-4 gather).  Per centre c = 1 .. k-1, three
+// stream-ordered launches:
+//   k_kpp_search  L blocks: target t's original-order weight block by an exact
+//                 prefix over the block sums `bsum`, then the first row of that
+//                 block whose inclusive prefix reaches the target (searchsorted
+//                 side='left'); extra blocks reduce the per-cell maxima of
+//                 `closest` to gmax (a bound on every point's closest distance)
+//   k_kpp_eval    per candidate, the potential drop sum_i w(closest_i) -
+//                 w(min(closest_i, d(x_i, cand))) over the cells the candidate
+//                 can reach: cells of the cube of radius sqrt(gmax) around it
+//                 whose box lower bound on the fp32 distance is below the cell's
+//                 max closest -- every other point's term is exactly 0
+//   k_kpp_apply   the first argmin of the potentials becomes centre c; the
+//                 closest distances, cell maxima and block sums of the cells it
+//                 reaches are updated
+// so a step touches only the neighbourhood of its L + 1 candidates (early
+// steps, with gmax large, are full passes).  Potentials are exact unsigned
+// integers: the sampled indices are the oracle's for any launch geometry.
 #pragma once
 #include "pcm_kernels.hpp"
 
 namespace pcm {
 
 constexpr int KPP_LMAX = 16;
-constexpr int KPP_BS = 8192;     // points per pass block (256 threads x 32)
+constexpr int KPP_OB_LOG = 12;                 // original-order weight blocks of 4096 rows
+constexpr int KPP_OB = 1 << KPP_OB_LOG;
+constexpr int KPP_CELL_PTS = 256;              // target points per pruning cell
+constexpr int KPP_STPB = 1024;                 // k_kpp_search block size
+constexpr int KPP_RED_BLOCKS = 64;             // gmax reduction blocks of k_kpp_search
 
-struct KppState {
-    float4 best;                  // centre chosen at the previous step
-    float4 cand[KPP_LMAX];        // this step's candidates
+struct KppCtl {
+    float4 cand[KPP_LMAX];
     long long cand_idx[KPP_LMAX];
-    long long loc_block[KPP_LMAX];
-    unsigned long long resid[KPP_LMAX];
-    unsigned long long pot;
-    int Lc, has_best, first, pad_;
+    unsigned long long pot[2];                 // potential at the start of step c: pot[c & 1]
+    unsigned long long delta[KPP_LMAX];        // potential drop of each candidate (k_kpp_eval)
+    unsigned int gmax_acc[2];                  // float bits: max closest, reduced by step c's search into [c & 1]
 };
 
+// w = trunc(ldexp(double(d), s)) for d >= 0, from the fp32 fields with integer
+// ops (exact: d = mant * 2^e2 before scaling; w < 2^64 by the choice of s).
 __device__ __forceinline__ unsigned long long kpp_w(float d, int s) {
-    return (unsigned long long)__builtin_ldexp((double)d, s);   // d >= 0: truncation
+    const unsigned bits = __float_as_uint(d);
+    const int E = (int)(bits >> 23);
+    const unsigned long long mant = (unsigned long long)((bits & 0x7fffffu) | (E ? 0x800000u : 0u));
+    const int e2 = (E ? E - 150 : -149) + s;
+    if (e2 >= 0) return mant << e2;
+    return e2 > -64 ? mant >> (-e2) : 0ull;
 }
 
 template <int D>
-__device__ __forceinline__ float4 row4(const float *X, long long i) {
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
+__device__ __forceinline__ void kpp_point(const float *__restrict__ xs, long long i, float (&x)[D]) {
 #pragma unroll
-    for (int a = 0; a < D; ++a) v[a] = X[i * D + a];
-    return make_float4(v[0], v[1], v[2], v[3]);
+    for (int a = 0; a < D; ++a) x[a] = xs[xs_index<D>(i, a)];
 }
 
+// Conservative reach test: true iff some point of the cell may have a
+// canonical fp32 distance to c strictly below cmax (the cell's max closest).
 template <int D>
-__device__ __forceinline__ float kdist(const float *X, long long i, const float4 &c) {
-    float x[D];
+__device__ __forceinline__ bool kpp_reaches(const Grid &g, long long cell, const float4 &c, float cmax) {
+    int f[MAXD];
+    decode(cell, g.G, D, f);
+    double blo[MAXD], bhi[MAXD];
+    cell_box<D>(g, f, f, blo, bhi);
+    double m = 0.0;
 #pragma unroll
-    for (int a = 0; a < D; ++a) x[a] = X[i * D + a];
-    return dist_canon<D>(x, c);
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void k_kpp_pass(const float *__restrict__ X, long long n, float *__restrict__ closest,
-                                                  const KppState *__restrict__ st, int s,
-                                                  unsigned long long *__restrict__ bsum) {
-    const int tid = threadIdx.x;
-    const long long b0 = (long long)blockIdx.x * KPP_BS;
-    const int Lc = st->Lc;
-    const bool first = st->first != 0, has_best = st->has_best != 0;
-    const float4 best = st->best;
-    float4 cand[KPP_LMAX];
-#pragma unroll
-    for (int l = 0; l < KPP_LMAX; ++l) cand[l] = st->cand[l];
-    unsigned long long acc[KPP_LMAX];
-#pragma unroll
-    for (int l = 0; l < KPP_LMAX; ++l) acc[l] = 0ull;
-    for (int e = tid; e < KPP_BS; e += 256) {
-        const long long i = b0 + e;
-        if (i >= n) break;
-        float x[D];
-#pragma unroll
-        for (int a = 0; a < D; ++a) x[a] = X[i * D + a];
-        float cl = first ? __builtin_inff() : closest[i];
-        if (has_best) cl = fminf(cl, dist_canon<D>(x, best));
-        closest[i] = cl;
-#pragma unroll
-        for (int l = 0; l < KPP_LMAX; ++l)
-            if (l < Lc) acc[l] += kpp_w(fminf(cl, dist_canon<D>(x, cand[l])), s);
+    for (int a = 0; a < D; ++a) {
+        const double ca = (double)comp(c, a);
+        const double t = ca < blo[a] ? blo[a] - ca : (ca > bhi[a] ? ca - bhi[a] : 0.0);
+        m += t * t;
     }
-    __shared__ unsigned long long red[KPP_LMAX][4];
-    const int lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-    for (int l = 0; l < KPP_LMAX; ++l) {
-        if (l >= Lc) break;
-        unsigned long long v = acc[l];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == 0) red[l][wv] = v;
-    }
-    __syncthreads();
-    if (tid < Lc) bsum[(size_t)blockIdx.x * KPP_LMAX + tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+    // d~ >= d (1 - 5u) - 3 * 2^-150 (DESIGN.md "Exactness of pruning")
+    return m * (1.0 - PEPS) - PTAU < (double)cmax;
 }
 
-// One block of 1024 threads.  umant: the next step's L uniforms as exact
-// 53-bit mantissas (nullptr after the last centre).
-__global__ __launch_bounds__(1024) void k_kpp_select(const unsigned long long *__restrict__ bsum, long long nblk,
-                                                     KppState *__restrict__ st, long long *__restrict__ indices,
-                                                     int c, const unsigned long long *__restrict__ umant, int Lnext) {
+// Cell-index cube around c of half-width sqrt(gmax) (+ one cell of binning slack).
+template <int D>
+__device__ __forceinline__ void kpp_cube(const Grid &g, const float4 &c, float gmax, int (&i0)[MAXD], int (&i1)[MAXD],
+                                         long long &vol) {
+    const double R = sqrt((double)gmax * (1.0 + 1.52587890625e-05) + 1e-36);
+    vol = 1;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        if (g.G[a] <= 1 || !(g.inv[a] > 0.0)) {
+            i0[a] = 0;
+            i1[a] = g.G[a] - 1;
+        } else {
+            const double ca = (double)comp(c, a);
+            const double lo = floor((ca - R - g.lo[a]) * g.inv[a]) - 1.0, hi = floor((ca + R - g.lo[a]) * g.inv[a]) + 1.0;
+            i0[a] = lo < 0.0 ? 0 : (lo > (double)(g.G[a] - 1) ? g.G[a] - 1 : (int)lo);
+            i1[a] = hi < 0.0 ? 0 : (hi > (double)(g.G[a] - 1) ? g.G[a] - 1 : (int)hi);
+        }
+        vol *= (long long)(i1[a] - i0[a] + 1);
+    }
+}
+
+template <int D>
+__device__ __forceinline__ long long kpp_cube_cell(const Grid &g, const int (&i0)[MAXD], const int (&i1)[MAXD],
+                                                   long long local) {
+    int f[MAXD];
+#pragma unroll
+    for (int a = D - 1; a >= 0; --a) {
+        const int w = i1[a] - i0[a] + 1;
+        f[a] = i0[a] + (int)(local % w);
+        local /= w;
+    }
+    return encode(f, g.G, D);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max_f(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Step 0: closest := d(x, c0) for every point, cell maxima, original-order
+// block sums of the weights and the potential.  One wave per cell (strided).
+template <int D>
+__global__ __launch_bounds__(256) void k_kpp_init(const float *__restrict__ xs, const uint32_t *__restrict__ perm,
+                                                  const uint32_t *__restrict__ cell_start, long long ncells,
+                                                  const float *__restrict__ X, long long first, int s,
+                                                  float *__restrict__ closest, float *__restrict__ cmax,
+                                                  unsigned long long *__restrict__ bsum, KppCtl *__restrict__ ctl,
+                                                  long long *__restrict__ indices) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) indices[0] = first;
+    float c0v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < D; ++a) c0v[a] = X[first * D + a];
+    const float4 c0 = make_float4(c0v[0], c0v[1], c0v[2], c0v[3]);
+    const int lane = threadIdx.x & 63;
+    const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    unsigned long long pot = 0ull;
+    for (long long cell = wid; cell < ncells; cell += nw) {
+        const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
+        float mx = 0.f;
+        for (uint32_t i = b + lane; i < e; i += 64) {
+            float x[D];
+            kpp_point<D>(xs, i, x);
+            const float d = dist_canon<D>(x, c0);
+            closest[i] = d;
+            const unsigned long long w = kpp_w(d, s);
+            pot += w;
+            atomicAdd(&bsum[perm[i] >> KPP_OB_LOG], w);
+            mx = fmaxf(mx, d);
+        }
+        mx = wave_max_f(mx);
+        if (lane == 0) cmax[cell] = mx;
+    }
+    pot = wave_sum_u64(pot);
+    if (lane == 0 && pot) atomicAdd(&ctl->pot[1], pot);
+}
+
+// Inclusive scan of one u64 per thread over a KPP_STPB-thread block: wave
+// scans (shfl_up), one LDS pass over the wave totals.  Returns the EXCLUSIVE
+// prefix of this thread.
+__device__ __forceinline__ unsigned long long kpp_block_exscan(unsigned long long v, unsigned long long *wtot) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int Lc = st->Lc;
-    __shared__ unsigned long long wp[16][KPP_LMAX];
-    __shared__ unsigned long long tsum[1024];
-    __shared__ int s_best;
-    // potentials (exact integer sums: any order)
-    unsigned long long p[KPP_LMAX];
-#pragma unroll
-    for (int l = 0; l < KPP_LMAX; ++l) p[l] = 0ull;
-    for (long long b = tid; b < nblk; b += 1024)
-#pragma unroll
-        for (int l = 0; l < KPP_LMAX; ++l)
-            if (l < Lc) p[l] += bsum[(size_t)b * KPP_LMAX + l];
-#pragma unroll
-    for (int l = 0; l < KPP_LMAX; ++l) {
-        unsigned long long v = p[l];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == 0) wp[wv][l] = v;
+    unsigned long long inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long u = __shfl_up(inc, o);
+        if (lane >= o) inc += u;
     }
+    if (lane == 63) wtot[wv] = inc;
     __syncthreads();
-    if (tid == 0) {
-        unsigned long long bp = 0ull;
-        int bl = -1;
-        for (int l = 0; l < Lc; ++l) {
-            unsigned long long v = 0ull;
-            for (int w = 0; w < 16; ++w) v += wp[w][l];
-            if (bl < 0 || v < bp) { bp = v; bl = l; }   // first argmin (np.argmin)
-        }
-        s_best = bl;
-        st->pot = bp;
-        st->best = st->cand[bl];
-        st->has_best = 1;
-        st->first = 0;
-        indices[c] = st->cand_idx[bl];
-    }
+    unsigned long long base = 0ull;
+    for (int w = 0; w < wv; ++w) base += wtot[w];
     __syncthreads();
-    if (!umant) return;
-    const int bl = s_best;
-    const unsigned long long pot = st->pot;
-    // thread tid owns the contiguous block range [b0, b1)
-    const long long per = (nblk + 1023) / 1024;
-    const long long b0 = tid * per < nblk ? tid * per : nblk, b1 = b0 + per < nblk ? b0 + per : nblk;
-    unsigned long long loc = 0ull;
-    for (long long b = b0; b < b1; ++b) loc += bsum[(size_t)b * KPP_LMAX + bl];
-    tsum[tid] = loc;
-    __syncthreads();
-    // inclusive scan of the thread sums (Hillis-Steele in LDS)
-    for (int o = 1; o < 1024; o <<= 1) {
-        const unsigned long long v = tid >= o ? tsum[tid - o] : 0ull;
-        __syncthreads();
-        tsum[tid] += v;
-        __syncthreads();
-    }
-    unsigned long long run = tsum[tid] - loc;   // exclusive prefix of this thread's range
-    for (int t = 0; t < Lnext; ++t) {
-        const unsigned long long m = umant[t];
-        const unsigned long long lo = m * pot, hi = __umul64hi(m, pot);
-        const unsigned long long tg = (hi << 11) | (lo >> 53);   // floor(u * pot)
-        // first block b with inclusive prefix >= tg (np.searchsorted side='left')
-        unsigned long long r = run;
-        for (long long b = b0; b < b1; ++b) {
-            const unsigned long long v = bsum[(size_t)b * KPP_LMAX + bl];
-            if (r + v >= tg && (b == 0 || r < tg)) {
-                st->loc_block[t] = b;
-                st->resid[t] = tg - r;
-            }
-            r += v;
-        }
-        if (tid == 1023 && r < tg) {   // past the end: np.searchsorted -> n, clipped to n-1
-            st->loc_block[t] = -1;
-            st->resid[t] = 0ull;
-        }
-    }
-    if (tid == 0) st->Lc = Lnext;
+    return base + inc - v;
 }
 
+// Step c (>= 1): blocks t < L locate candidate t; blocks >= L reduce gmax.
 template <int D>
-__global__ void k_kpp_init(const float *__restrict__ X, long long first, KppState *__restrict__ st) {
-    if (threadIdx.x != 0) return;
-    st->cand[0] = row4<D>(X, first);
-    st->cand_idx[0] = first;
-    st->Lc = 1;
-    st->first = 1;
-    st->has_best = 0;
-    st->pot = 0ull;
-}
-
-// One block (1024 threads) per target: the exact index inside its block.
-template <int D>
-__global__ __launch_bounds__(1024) void k_kpp_locate(const float *__restrict__ X, long long n,
-                                                     const float *__restrict__ closest, KppState *__restrict__ st,
-                                                     int s) {
-    const int t = blockIdx.x, tid = threadIdx.x;
-    const long long b = st->loc_block[t];
-    if (b < 0) {
-        if (tid == 0) {
-            st->cand_idx[t] = n - 1;
-            st->cand[t] = row4<D>(X, n - 1);
-        }
+__global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long long *__restrict__ bsum, long long nb,
+                                                         const float *__restrict__ closest,
+                                                         const uint32_t *__restrict__ inv, const float *__restrict__ X,
+                                                         long long n, const unsigned long long *__restrict__ umant,
+                                                         int L, int s, int c, const float *__restrict__ cmax,
+                                                         long long ncells, KppCtl *__restrict__ ctl) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    if ((int)blockIdx.x >= L) {   // gmax: max over the cells' max closest
+        unsigned int m = 0u;
+        for (long long cl = (blockIdx.x - L) * (long long)KPP_STPB + tid; cl < ncells;
+             cl += (long long)(gridDim.x - L) * KPP_STPB)
+            m = max(m, __float_as_uint(cmax[cl]));
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o));
+        if (lane == 0 && m) atomicMax(&ctl->gmax_acc[c & 1], m);
         return;
     }
-    const unsigned long long rs = st->resid[t];
-    const float4 best = st->best;
-    constexpr int PER = KPP_BS / 1024;   // 8 consecutive points per thread
-    unsigned long long w[PER], loc = 0ull;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-        const long long i = b * KPP_BS + (long long)tid * PER + e;
-        w[e] = i < n ? kpp_w(fminf(closest[i], kdist<D>(X, i, best)), s) : 0ull;
-        loc += w[e];
+    const int t = blockIdx.x;
+    if (t == 0)
+        for (int l = tid; l < KPP_LMAX; l += KPP_STPB) ctl->delta[l] = 0ull;
+    __shared__ unsigned long long wtot[KPP_STPB / 64];
+    __shared__ long long s_blk;
+    __shared__ unsigned long long s_res;
+    __shared__ long long s_found;
+    const unsigned long long pot = ctl->pot[c & 1];
+    const unsigned long long m = umant[t];
+    const unsigned long long lo = m * pot, hi = __umul64hi(m, pot);
+    const unsigned long long tg = (hi << 11) | (lo >> 53);   // floor(u * pot), u = m / 2^53
+    if (tid == 0) { s_blk = -1; s_found = 0x7fffffffffffffffll; }
+    // 1. original-order block containing the target: thread tid owns blocks [b0, b1)
+    const long long per = (nb + KPP_STPB - 1) / KPP_STPB;
+    const long long b0 = min((long long)tid * per, nb), b1 = min(b0 + per, nb);
+    unsigned long long loc = 0ull;
+    for (long long b = b0; b < b1; ++b) loc += bsum[b];
+    unsigned long long r = kpp_block_exscan(loc, wtot);   // exclusive prefix of this thread's range
+    for (long long b = b0; b < b1; ++b) {
+        const unsigned long long v = bsum[b];
+        if (r + v >= tg && (b == 0 || r < tg)) {   // first block whose inclusive prefix reaches tg
+            s_blk = b;
+            s_res = tg - r;
+        }
+        r += v;
     }
-    __shared__ unsigned long long tsum[1024];
-    __shared__ long long found;
-    if (tid == 0) found = 0x7fffffffffffffffll;
-    tsum[tid] = loc;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const unsigned long long v = tid >= o ? tsum[tid - o] : 0ull;
-        __syncthreads();
-        tsum[tid] += v;
-        __syncthreads();
-    }
-    unsigned long long r = tsum[tid] - loc;
+    const long long blk = s_blk;
+    long long idx = n - 1;   // past the end (np.searchsorted -> n, clipped): not reachable, tg < pot
+    if (blk >= 0) {
+        // 2. first row of the block whose inclusive prefix reaches the residual
+        const unsigned long long rs = s_res;
+        constexpr int PER = KPP_OB / KPP_STPB;
+        unsigned long long w[PER];
+        unsigned long long l2 = 0ull;
 #pragma unroll
-    for (int e = 0; e < PER; ++e) {
-        const long long i = b * KPP_BS + (long long)tid * PER + e;
-        if (i < n && r + w[e] >= rs) atomicMin(&found, i);   // first inclusive prefix >= rs
-        r += w[e];
+        for (int e = 0; e < PER; ++e) {
+            const long long j = blk * KPP_OB + (long long)tid * PER + e;
+            w[e] = j < n ? kpp_w(closest[inv[j]], s) : 0ull;
+            l2 += w[e];
+        }
+        unsigned long long q = kpp_block_exscan(l2, wtot);
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+            const long long j = blk * KPP_OB + (long long)tid * PER + e;
+            if (j < n && q + w[e] >= rs) atomicMin(&s_found, j);
+            q += w[e];
+        }
+        __syncthreads();
+        idx = s_found < n ? s_found : n - 1;
+    }
+    if (tid == 0) {
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < D; ++a) v[a] = X[idx * D + a];
+        ctl->cand[t] = make_float4(v[0], v[1], v[2], v[3]);
+        ctl->cand_idx[t] = idx;
+    }
+}
+
+// Step c: potential drop of every candidate over the cells it reaches.  While
+// the candidates' cubes together cover more items than the grid has cells
+// (early steps), every wave walks whole cells and evaluates all reaching
+// candidates on one load of each point; later, one wave per (candidate, cube
+// cell) item.  Per-lane, per-candidate partial sums in registers, one wave
+// reduction and atomic per candidate at the end.
+template <int D>
+__global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, const uint32_t *__restrict__ cell_start,
+                                                  Grid g, const float *__restrict__ closest,
+                                                  const float *__restrict__ cmax, int L, int s, int c,
+                                                  KppCtl *__restrict__ ctl) {
+    __shared__ int s_i0[KPP_LMAX][MAXD], s_i1[KPP_LMAX][MAXD];
+    __shared__ long long s_off[KPP_LMAX + 1];
+    __shared__ float4 s_cand[KPP_LMAX];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const float gmax = __uint_as_float(ctl->gmax_acc[c & 1]);
+    if (tid < L) {
+        const float4 cd = ctl->cand[tid];
+        int i0[MAXD], i1[MAXD];
+        long long vol;
+        kpp_cube<D>(g, cd, gmax, i0, i1, vol);
+#pragma unroll
+        for (int a = 0; a < D; ++a) { s_i0[tid][a] = i0[a]; s_i1[tid][a] = i1[a]; }
+        s_off[tid + 1] = vol;
+        s_cand[tid] = cd;
     }
     __syncthreads();
     if (tid == 0) {
-        long long i = found;
-        if (i >= n) i = n - 1;
-        st->cand_idx[t] = i;
-        st->cand[t] = row4<D>(X, i);
+        s_off[0] = 0;
+        for (int l = 0; l < L; ++l) s_off[l + 1] += s_off[l];
+    }
+    __syncthreads();
+    const long long total = s_off[L];
+    const long long wid = (blockIdx.x * (long long)blockDim.x + tid) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    unsigned long long dw[KPP_LMAX];
+#pragma unroll
+    for (int q = 0; q < KPP_LMAX; ++q) dw[q] = 0ull;
+    if (total > g.ncells) {
+        for (long long cell = wid; cell < g.ncells; cell += nw) {
+            const float cm = cmax[cell];
+            const bool reach = lane < L && kpp_reaches<D>(g, cell, s_cand[lane < L ? lane : 0], cm);
+            const unsigned mask = (unsigned)__ballot(reach);
+            if (!mask) continue;   // wave-uniform
+            const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
+            for (uint32_t i = b + lane; i < e; i += 64) {
+                float x[D];
+                kpp_point<D>(xs, i, x);
+                const float cl = closest[i];
+                const unsigned long long wcl = kpp_w(cl, s);
+#pragma unroll
+                for (int q = 0; q < KPP_LMAX; ++q) {
+                    if (!((mask >> q) & 1u)) continue;
+                    const float d = dist_canon<D>(x, s_cand[q]);
+                    if (d < cl) dw[q] += wcl - kpp_w(d, s);
+                }
+            }
+        }
+    } else {
+        int l = 0;
+        for (long long it = wid; it < total; it += nw) {
+            while (it >= s_off[l + 1]) ++l;   // items ascend per wave
+            int i0[MAXD], i1[MAXD];
+#pragma unroll
+            for (int a = 0; a < D; ++a) { i0[a] = s_i0[l][a]; i1[a] = s_i1[l][a]; }
+            const long long cell = kpp_cube_cell<D>(g, i0, i1, it - s_off[l]);
+            const float4 cd = s_cand[l];
+            if (!kpp_reaches<D>(g, cell, cd, cmax[cell])) continue;   // wave-uniform
+            const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
+            unsigned long long v = 0ull;
+            for (uint32_t i = b + lane; i < e; i += 64) {
+                float x[D];
+                kpp_point<D>(xs, i, x);
+                const float d = dist_canon<D>(x, cd);
+                const float cl = closest[i];
+                if (d < cl) v += kpp_w(cl, s) - kpp_w(d, s);
+            }
+#pragma unroll
+            for (int q = 0; q < KPP_LMAX; ++q)
+                if (q == l) dw[q] += v;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < KPP_LMAX; ++q) {
+        if (q >= L) break;
+        const unsigned long long v = wave_sum_u64(dw[q]);
+        if (lane == 0 && v) atomicAdd(&ctl->delta[q], v);
+    }
+}
+
+// Step c: select (first argmin of the candidates' potentials) and, unless this
+// is the last centre, apply the new centre to the cells it reaches.
+template <int D>
+__global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs, const uint32_t *__restrict__ perm,
+                                                   const uint32_t *__restrict__ cell_start, Grid g,
+                                                   float *__restrict__ closest, float *__restrict__ cmax,
+                                                   unsigned long long *__restrict__ bsum, int L, int s, int c,
+                                                   int apply, long long *__restrict__ indices,
+                                                   KppCtl *__restrict__ ctl) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const unsigned long long pot = ctl->pot[c & 1];
+    int bl = 0;
+    unsigned long long bp = pot - ctl->delta[0];
+    for (int q = 1; q < L; ++q) {
+        const unsigned long long v = pot - ctl->delta[q];
+        if (v < bp) { bp = v; bl = q; }   // first argmin (np.argmin)
+    }
+    const float4 best = ctl->cand[bl];
+    const float gmax = __uint_as_float(ctl->gmax_acc[c & 1]);
+    if (blockIdx.x == 0 && tid == 0) {
+        indices[c] = ctl->cand_idx[bl];
+        ctl->pot[(c + 1) & 1] = bp;
+        ctl->gmax_acc[(c + 1) & 1] = 0u;
+    }
+    if (!apply) return;
+    int i0[MAXD], i1[MAXD];
+    long long vol;
+    kpp_cube<D>(g, best, gmax, i0, i1, vol);
+    const long long wid = (blockIdx.x * (long long)blockDim.x + tid) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    for (long long it = wid; it < vol; it += nw) {
+        const long long cell = kpp_cube_cell<D>(g, i0, i1, it);
+        if (!kpp_reaches<D>(g, cell, best, cmax[cell])) continue;   // wave-uniform
+        const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
+        float mx = 0.f;
+        for (uint32_t i = b + lane; i < e; i += 64) {
+            float x[D];
+            kpp_point<D>(xs, i, x);
+            const float d = dist_canon<D>(x, best);
+            const float cl = closest[i];
+            if (d < cl) {
+                closest[i] = d;
+                atomicAdd(&bsum[perm[i] >> KPP_OB_LOG], ~(kpp_w(cl, s) - kpp_w(d, s)) + 1ull);   // -= (mod 2^64)
+            }
+            mx = fmaxf(mx, fminf(d, cl));
+        }
+        mx = wave_max_f(mx);
+        if (lane == 0) cmax[cell] = mx;
     }
 }
 

@@ -21,7 +21,8 @@ from .engine import _ptr, _stream
 
 
 def _scale(n: int, maxd: float) -> int:
-    """Weight exponent: n * 2**s * maxd (with rounding margin) < 2**62."""
+    """Weight exponent: n * 2**s * maxd (with rounding margin) < 2**62 (computed
+    again by pcm_kmeanspp from the device bounding box; kept for the tests)."""
     if maxd <= 0 or n <= 0:
         return 0
     _, e = math.frexp(maxd * (1.0 + 2.0 ** -20))
@@ -30,12 +31,23 @@ def _scale(n: int, maxd: float) -> int:
 
 def _first_index(n: int, u0: float) -> int:
     """numpy RandomState.choice(n, p=w / w.sum()) for its single random_sample() draw u0,
-    with sklearn's unit float32 weights (``_check_sample_weight`` in X's dtype)."""
-    w = np.ones(n, dtype=np.float32)
-    p = (w / w.sum()).astype(np.float64)
-    cdf = p.cumsum()
-    cdf /= cdf[-1]
-    return int(cdf.searchsorted(u0, side="right"))
+    with sklearn's unit float32 weights (``_check_sample_weight`` in X's dtype).
+
+    choice() searches u0 (side='right') in cdf = cumsum(p) / cumsum(p)[-1] with
+    p[i] = v (one float32 constant widened to float64).  For n < 2**29 every
+    partial sum (i + 1) * v is exact in float64 (v has 24 significant bits), so
+    cdf[i] = RN((i + 1) / n) whatever v is: the index is the first i with
+    RN((i + 1) / n) > u0 -- O(1) instead of three n-element float64 arrays."""
+    if n >= 2 ** 29:
+        w = np.ones(n, dtype=np.float32)
+        p = (w / w.sum()).astype(np.float64)
+        cdf = p.cumsum()
+        cdf /= cdf[-1]
+        return int(cdf.searchsorted(u0, side="right"))
+    i = max(0, int(u0 * n) - 2)
+    while i < n and (i + 1) / n <= u0:     # Python float division rounds correctly
+        i += 1
+    return min(i, n - 1)
 
 
 def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_local_trials=None):
@@ -49,8 +61,6 @@ def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_lo
     k = int(n_clusters)
     if not 1 <= k <= n:
         raise ValueError(f"n_samples={n} should be >= n_clusters={k}")
-    if not torch.isfinite(Xf).all():
-        raise ValueError("input points contain NaN or Inf")
     rs = random_state if isinstance(random_state, np.random.RandomState) else np.random.RandomState(random_state)
     L = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
     u0 = rs.random_sample()
@@ -60,11 +70,16 @@ def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_lo
         m = np.ldexp(u, 53)
         assert np.array_equal(np.ldexp(m, -53), u)      # random_sample doubles are multiples of 2**-53
         umant[(c - 1) * L:c * L] = m.astype(np.uint64)
-    ext = Xf.amax(0).double() - Xf.amin(0).double()
-    s = _scale(n, float((ext * ext).sum()))
     first = _first_index(n, u0)
     idx = torch.empty(k, dtype=torch.int64, device=Xf.device)
     lib = _lib.load()
-    _lib.check(lib.pcm_kmeanspp(_ptr(Xf), n, d, k, L, first, umant.ctypes.data_as(ctypes.c_void_p), s, _ptr(idx),
-                                _stream()), "pcm_kmeanspp")
+    nbytes = ctypes.c_size_t()
+    _lib.check(lib.pcm_kmeanspp_workspace(n, d, k, L, ctypes.byref(nbytes)), "pcm_kmeanspp_workspace")
+    # device workspace from torch's caching allocator (reused by later calls)
+    ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=Xf.device)
+    rc = lib.pcm_kmeanspp(_ptr(Xf), n, d, k, L, first, umant.ctypes.data_as(ctypes.c_void_p), _ptr(idx), _ptr(ws),
+                          nbytes.value, _stream())
+    if rc == -4:
+        raise ValueError("input points contain NaN or Inf")
+    _lib.check(rc, "pcm_kmeanspp")
     return Xf[idx].clone(), idx

@@ -115,7 +115,8 @@ def main():
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--d", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--fit", action="store_true", help="also time GPU k-means++ seeding of the bench cloud")
+    ap.add_argument("--fit", "--kpp", dest="fit", action="store_true",
+                    help="also time GPU k-means++ seeding (K centres) of the bench cloud")
     ap.add_argument("--fit-iters", type=int, default=20, help="iterations of the timed whole fit (0: skip)")
     ap.add_argument("--split", action="store_true",
                     help="one GPU through the multi-GPU call sequence (nccl group of 1; calibration)")

@@ -40,7 +40,9 @@ extern "C" {
 
 #define PCM_ABI_VERSION 2
 
-enum pcm_dtype { PCM_F32 = 0, PCM_F16 = 1 };
+enum pcm_dtype { PCM_F32 = 0, PCM_F16 = 1, PCM_F64 = 2 /* dense path only */ };
+
+#define PCM_DENSE_DMAX 64   /* features of the generic-D (dense) path */
 
 enum pcm_err {
     PCM_OK = 0,
@@ -179,11 +181,14 @@ int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int 
  * (row order = the caller's); first_index: the first centre (sklearn's
  * random_state.choice draw, computed by the host); umant: host uint64
  * [(k-1)*n_local_trials], each uniform of random_state.uniform(size=L) for
- * centres 1..k-1 as its exact 53-bit mantissa (u * 2^53); scale: weight
- * exponent s (kpp_scale).  Writes indices (device int64[k]) and synchronises
- * the stream before returning (allocates a per-call workspace). */
+ * centres 1..k-1 as its exact 53-bit mantissa (u * 2^53).  The weight
+ * exponent is kpp_scale(n, sum_a (max_a - min_a)^2) of the device bounding box.
+ * Writes indices (device int64[k]), stream-ordered; synchronises once (bounding
+ * box -> pruning grid) and returns PCM_E_NONFINITE for NaN/Inf input.
+ * workspace: caller-owned device memory of pcm_kmeanspp_workspace bytes. */
+int pcm_kmeanspp_workspace(int64_t n, int d, int k, int n_local_trials, size_t *bytes);
 int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, int64_t first_index,
-                 const uint64_t *umant, int scale, int64_t *indices, void *stream);
+                 const uint64_t *umant, int64_t *indices, void *workspace, size_t workspace_bytes, void *stream);
 
 /* Per-pair point-cloud assembly, replacing the float64 NumPy block of
  * members/rafael/disparity/plugin.py:147-192 (height = -disparity/16, validity
@@ -195,6 +200,39 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
  * double[3], nullable) = the fitted plane normal.  Synchronises the stream. */
 int pcm_cloud_assemble(const double *disparity, const uint8_t *validity, int64_t H, int64_t W, double limit,
                        double *points, double *hnorm, int64_t *m_out, double *normal_out, void *stream);
+
+/* ---------------------------------------------------------------- dense path
+ * Generic-D Lloyd K-means for feature vectors (D <= PCM_DENSE_DMAX, float32 or
+ * float64, computed in that precision), replacing one _kmeans_single_lloyd
+ * call (sklearn/cluster/_kmeans.py:623-752) at the reference's KMeans call site
+ * members/jasraj/land_use_classification/core.py:227-228 (~1500 x 20 float64).
+ * Brute force over all K with the centres staged in LDS (k*d*sizeof <= 64 KB);
+ * canonical arithmetic of oracle/dense_ref.py; everything on the device, one
+ * process (no sharding).  X (device, n*d, row-major) must stay valid and
+ * unchanged from pcm_dense_begin to the last call of the fit.  maxabs (host
+ * double[d]) = max |X[:, a]| fixes the exact fixed-point sums. */
+typedef struct pcm_dense pcm_dense;
+int pcm_dense_create(int device, int64_t n, int d, int k, int dtype, int max_iter, pcm_dense **out);
+int pcm_dense_destroy(pcm_dense *e);
+/* centres C0: device k*d of dtype; labels := -1, history cleared (synchronises). */
+int pcm_dense_begin(pcm_dense *e, const void *X, const double *maxabs, const void *C0, double tol, int max_iter,
+                    void *stream);
+/* n_iter Lloyd iterations (E-step + update), gated on the device after convergence. */
+int pcm_dense_iterate(pcm_dense *e, int n_iter, void *stream);
+/* Final E-step with the final centres: labels + exact inertia limbs. */
+int pcm_dense_final(pcm_dense *e, void *stream);
+/* Status (synchronises): done/iter/last_*, inertia; list_rebuilds = relocation events. */
+int pcm_dense_status(pcm_dense *e, pcm_status *out, void *stream);
+/* Outputs (synchronises): labels device int32[n], centres device k*d dtype,
+ * history host uint64/double[cap]; any pointer may be NULL. */
+int pcm_dense_outputs(pcm_dense *e, int32_t *labels, void *centers, uint64_t *changed, double *shift, int cap,
+                      void *stream);
+/* k-means++ for the dense path (oracle/kpp_ref.py canonical seeding in the
+ * input precision), brute force; scale = kpp_scale(n, max distance bound). */
+int pcm_dense_kmeanspp_workspace(int64_t n, int d, int dtype, int k, int n_local_trials, size_t *bytes);
+int pcm_dense_kmeanspp(const void *X, int64_t n, int d, int dtype, int k, int n_local_trials, int64_t first_index,
+                       const uint64_t *umant, int scale, int64_t *indices, void *workspace, size_t workspace_bytes,
+                       void *stream);
 
 #ifdef __cplusplus
 }

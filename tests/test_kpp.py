@@ -41,6 +41,11 @@ def test_host_helpers_match_oracle():
     w = np.ones(1000, np.float32)
     assert K._first_index(1000, u0) == np.random.RandomState(3).choice(1000, p=w / w.sum())
     assert P.first_index(1000, u0) == K._first_index(1000, u0)
+    # the O(1) form equals numpy's cumsum/searchsorted (oracle) on awkward sizes and draws
+    rs = np.random.RandomState(11)
+    for n in (1, 2, 3, 7, 1000, 65537, 1_000_003, 3_000_000):
+        for u in list(rs.random_sample(6)) + [0.0, 1.0 - 2.0 ** -53, 0.5, 1.0 / 3.0]:
+            assert K._first_index(n, u) == P.first_index(n, u), (n, u)
 
 
 def test_weights_cannot_overflow():
@@ -63,10 +68,12 @@ def gpu():
 
 
 GPU_CASES = CASES + [
-    (50000, 32, 3, 9),          # several pass blocks (8192 points each), ragged tail
+    (50000, 32, 3, 9),          # several original-order weight blocks (4096 rows), ragged tail
     (100000, 64, 3, 1),
     (1000, 1000, 3, 2),         # k == n
     (1, 1, 3, 0),
+    (300000, 256, 3, 4),        # many cells: late steps touch only the candidates' neighbourhoods
+    (120000, 128, 4, 6),
 ]
 
 
@@ -102,4 +109,32 @@ def test_gpu_matches_sklearn(gpu):
     X = R.splitmix_uniform(8000, 3, seed=77)
     _, i_ref = sk.kmeans_plusplus(X, 24, random_state=123)
     _, i = pcm.kmeans_plusplus(torch.from_numpy(X).cuda(), 24, random_state=123)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+
+
+@pytest.mark.gpu
+def test_gpu_duplicates_and_clusters(gpu):
+    """Heavy duplication (zero potentials inside cells) and tight clusters far apart."""
+    torch, pcm = gpu
+    rng = np.random.default_rng(8)
+    centres = rng.uniform(-100, 100, size=(12, 3)).astype(np.float32)
+    X = (centres[rng.integers(0, 12, 60000)] + rng.normal(0, 0.05, (60000, 3))).astype(np.float32)
+    X[::7] = X[3]                      # a sixth of the cloud is one point
+    c_ref, i_ref = P.kmeanspp(X, 40, 17)
+    c, i = pcm.kmeans_plusplus(torch.from_numpy(X).cuda(), 40, random_state=17)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+
+
+@pytest.mark.gpu
+def test_gpu_heightmap_like(gpu):
+    """Anisotropic 2.5-D pixel-unit cloud (z, y, x as plugin.py:191-192 emits)."""
+    torch, pcm = gpu
+    rng = np.random.default_rng(9)
+    n = 150_000
+    y = rng.integers(0, 1800, n).astype(np.float64)
+    x = rng.integers(0, 2400, n).astype(np.float64)
+    z = 10 * np.sin(x / 200) + 5 * np.cos(y / 150) + rng.normal(0, 0.5, n) + 30
+    X = np.stack([z, y, x], axis=1).astype(np.float32)
+    c_ref, i_ref = P.kmeanspp(X, 96, 21)
+    c, i = pcm.kmeans_plusplus(torch.from_numpy(X).cuda(), 96, random_state=21)
     np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
