@@ -15,11 +15,15 @@ This class keeps that API and restates the control flow of scikit-learn 1.7.2's
   clustering differs (``_is_same_clustering``, ``_k_means_common.pyx:314-328``);
   ``n_init='auto'`` is 1 for k-means++ / an array, 10 for ``'random'``.
 
-Every pass over the cloud runs in the HIP kernels (k-means++ seeding, Lloyd
+Every pass over the data runs in the HIP kernels (k-means++ seeding, Lloyd
 iterations, final E-step); the host holds only O(K) state plus the mean/var of
-the boundary, which mirror sklearn's own NumPy calls.  Arithmetic is the
-canonical float32 form of DESIGN.md §2 (sklearn keeps float64 input in
-float64; here it is rounded to float32 at the boundary).
+the boundary, which mirror sklearn's own NumPy calls.  Dtypes follow sklearn
+(float32 stays float32, everything else becomes float64):
+
+* float32 point clouds (D <= 4): the pruned point-cloud engine (``lloyd_fit``,
+  ``kmeans_plusplus``; canonical float32 arithmetic, DESIGN.md §2);
+* float64 input or D > 4 (the reference's 1500 x 20 float64 call site): the
+  dense engine (``dense.py``), computing in the input precision.
 """
 from __future__ import annotations
 
@@ -54,12 +58,21 @@ class KMeans:
 
     # ------------------------------------------------------------ GPU legs
     @staticmethod
+    def _dense(X: np.ndarray) -> bool:
+        return X.dtype == np.float64 or X.shape[1] > 4
+
+    @staticmethod
     def _gpu_fit(Xc: np.ndarray, C0: np.ndarray, max_iter: int, tol: float):
         import torch
 
-        from .lloyd import LOCAL, lloyd_fit
-        res = lloyd_fit(torch.from_numpy(Xc).cuda(), torch.from_numpy(np.ascontiguousarray(C0, np.float32)).cuda(),
-                        max_iter=max_iter, tol=tol, group=LOCAL)
+        if KMeans._dense(Xc):
+            from .dense import dense_fit
+            res = dense_fit(torch.from_numpy(Xc).cuda(), torch.from_numpy(np.ascontiguousarray(C0, Xc.dtype)).cuda(),
+                            max_iter=max_iter, tol=tol)
+        else:
+            from .lloyd import LOCAL, lloyd_fit
+            res = lloyd_fit(torch.from_numpy(Xc).cuda(), torch.from_numpy(np.ascontiguousarray(C0, np.float32)).cuda(),
+                            max_iter=max_iter, tol=tol, group=LOCAL)
         torch.cuda.synchronize()
         return res.labels.cpu().numpy(), res.centers.cpu().numpy(), float(res.inertia), int(res.n_iter)
 
@@ -67,8 +80,12 @@ class KMeans:
     def _gpu_seed(Xc: np.ndarray, k: int, rs: np.random.RandomState) -> np.ndarray:
         import torch
 
-        from .kpp import kmeans_plusplus
-        C, _ = kmeans_plusplus(torch.from_numpy(Xc).cuda(), k, random_state=rs)
+        if KMeans._dense(Xc):
+            from .dense import dense_kmeanspp
+            C, _ = dense_kmeanspp(torch.from_numpy(Xc).cuda(), k, random_state=rs)
+        else:
+            from .kpp import kmeans_plusplus
+            C, _ = kmeans_plusplus(torch.from_numpy(Xc).cuda(), k, random_state=rs)
         return C.cpu().numpy()
 
     # ------------------------------------------------------------ sklearn API
@@ -79,7 +96,9 @@ class KMeans:
             raise NotImplementedError("algorithm='lloyd' only")
         if hasattr(X, "detach"):
             X = X.detach().cpu().numpy()
-        X = np.array(X, dtype=np.float32, order="C", copy=True)     # boundary: float32, C order
+        X = np.asarray(X)
+        dt = np.float32 if X.dtype == np.float32 else np.float64     # sklearn: dtype=[float64, float32]
+        X = np.array(X, dtype=dt, order="C", copy=True)
         n, d = X.shape
         k = int(self.n_clusters)
         if n < k:
@@ -92,8 +111,12 @@ class KMeans:
             n_init = int(self.n_init)
         if init_is_array and n_init != 1:
             n_init = 1    # sklearn warns and runs once for an explicit init array
-        rs = self.random_state if isinstance(self.random_state, np.random.RandomState) \
-            else np.random.RandomState(self.random_state)
+        if isinstance(self.random_state, np.random.RandomState):
+            rs = self.random_state
+        elif self.random_state is None:          # sklearn check_random_state(None): numpy's global RandomState
+            rs = np.random.mtrand._rand
+        else:
+            rs = np.random.RandomState(self.random_state)
         tol_abs = float(np.mean(np.var(X, axis=0)) * self.tol) if self.tol else 0.0   # _tolerance (X's dtype)
         X_mean = X.mean(axis=0)
         Xc = X - X_mean                                                              # centring (:1479-1484)
@@ -102,7 +125,7 @@ class KMeans:
         best = None
         for _ in range(n_init):
             if init_is_array:
-                C0 = np.asarray(init, dtype=np.float32) - X_mean
+                C0 = np.asarray(init, dtype=dt) - X_mean
             elif init == "k-means++":
                 C0 = seed(Xc, k, rs)
             elif init == "random":
@@ -114,9 +137,9 @@ class KMeans:
             if best is None or (inertia < best[2] and not _same_clustering(labels, best[0], k)):
                 best = (labels, centers, inertia, n_iter)
         labels, centers, inertia, n_iter = best
-        self.cluster_centers_ = (centers + X_mean).astype(np.float32)
+        self.cluster_centers_ = (centers + X_mean).astype(dt)
         self.labels_ = labels.astype(np.int32)
-        self.inertia_ = inertia
+        self.inertia_ = dt(inertia)           # sklearn returns the inertia in X's dtype
         self.n_iter_ = n_iter
         self.n_features_in_ = d
         return self

@@ -91,15 +91,22 @@ def draws(seed, k: int, L: int):
     return u0, us
 
 
-def kmeanspp(X, k: int, seed, n_local_trials: int | None = None):
-    """Returns (centers (k, d) float32, indices (k,) int64)."""
-    X = as_f32_points(X)
+def kmeanspp(X, k: int, seed, n_local_trials: int | None = None, keep_dtype: bool = False):
+    """Returns (centers (k, d), indices (k,) int64).  Distances in float32 (the
+    point-cloud path), or in X's own dtype when ``keep_dtype`` (the dense path,
+    oracle/dense_ref.py: float64 features stay float64 as in scikit-learn)."""
+    if keep_dtype:
+        X = np.ascontiguousarray(np.asarray(X))
+        if X.dtype not in (np.float32, np.float64):
+            X = X.astype(np.float64)
+    else:
+        X = as_f32_points(X)
     n, d = X.shape
     L = n_trials(k) if n_local_trials is None else int(n_local_trials)
     u0, us = draws(seed, k, L)
     s = kpp_scale(n, max_dist_bound(X))
     idx = np.full(k, -1, dtype=np.int64)
-    idx[0] = first_index(n, u0)
+    idx[0] = first_index(n, u0, X.dtype)
     closest = sqdist_rows(X, np.broadcast_to(X[idx[0]], X.shape))          # float32
     pot = int(weights(closest, s).sum(dtype=np.uint64))
     for c in range(1, k):
