@@ -10,6 +10,8 @@ lloyd_fit(X, centers_init, max_iter, tol, group=None)  -> LloydResult
 kmeans_plusplus(X, n_clusters, random_state=...)       -> (centers, indices), GPU k-means++
 assemble_cloud(disparity, validity, max_disp=288)      -> per-pair (z,y,x) cloud + height property (GPU)
 KMeans(n_clusters, init, n_init, ...).fit_predict(X)   -> the reference's KMeans call site (core.py:227-228)
+dense_fit / dense_kmeanspp                             -> generic-D (float32/float64) Lloyd + k-means++ (GPU)
+photoconsistency_map / left_right_consistency          -> stereo consistency gathers (GPU, processing.py / disparity.py)
 kmeans_fuse(clouds, n_clusters, ...)                   -> napari layer tuples
 HeightMapExtractor                                     -> SatellitePlugin drop-in
 Engine                                                 -> the C-ABI engine wrapper
@@ -18,7 +20,8 @@ from .fixed import QBITS, fixed_q  # noqa: F401
 from .lloyd import LloydResult, lloyd_fit  # noqa: F401
 
 __all__ = ["lloyd_fit", "LloydResult", "fixed_q", "QBITS", "Engine", "kmeans_fuse", "HeightMapExtractor",
-           "build_library", "kmeans_plusplus", "assemble_cloud", "KMeans"]
+           "build_library", "kmeans_plusplus", "assemble_cloud", "KMeans", "dense_fit", "dense_kmeanspp",
+           "photoconsistency_map", "left_right_consistency"]
 
 
 def __getattr__(name):
@@ -35,6 +38,12 @@ def __getattr__(name):
     if name == "assemble_cloud":
         from .cloud import assemble_cloud
         return assemble_cloud
+    if name in ("dense_fit", "dense_kmeanspp"):
+        from . import dense
+        return getattr(dense, name)
+    if name in ("photoconsistency_map", "left_right_consistency"):
+        from . import stereo
+        return getattr(stereo, name)
     if name == "kmeans_plusplus":
         from .kpp import kmeans_plusplus
         return kmeans_plusplus

@@ -14,7 +14,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 SO_PATH = os.environ.get("PCM_SO") or os.path.join(PKG_DIR, "libpcmkm.so")
-UNITS = [os.path.join(PKG_DIR, "csrc", "pcm_engine.hip"), os.path.join(PKG_DIR, "csrc", "pcm_dense.hip")]
+UNITS = [os.path.join(PKG_DIR, "csrc", u) for u in ("pcm_engine.hip", "pcm_dense.hip", "pcm_stereo.hip")]
 SOURCES = UNITS + [os.path.join(PKG_DIR, "csrc", h) for h in ("pcm_kernels.hpp", "pcm_kpp.hpp", "pcm_cloud.hpp",
                                                               "pcm_common.hpp")] + \
     [os.path.join(REPO_DIR, "include", "pcm_kmeans.h")]
@@ -31,6 +31,7 @@ EXPORTS = [
     "pcm_inertia_value", "pcm_kmeanspp_workspace",
     "pcm_dense_create", "pcm_dense_destroy", "pcm_dense_begin", "pcm_dense_iterate", "pcm_dense_final",
     "pcm_dense_status", "pcm_dense_outputs", "pcm_dense_kmeanspp_workspace", "pcm_dense_kmeanspp",
+    "pcm_photoconsistency", "pcm_lr_consistency",
 ]
 ABI_VERSION = 2
 
@@ -111,6 +112,8 @@ def _declare(lib):
         "pcm_dense_outputs": ([P, P, P, P, P, I, P], I),
         "pcm_dense_kmeanspp_workspace": ([I64, I, I, I, I, ctypes.POINTER(ctypes.c_size_t)], I),
         "pcm_dense_kmeanspp": ([P, I64, I, I, I, I, I64, P, I, P, P, ctypes.c_size_t, P], I),
+        "pcm_photoconsistency": ([P, P, I, P, I64, I64, D, P, P], I),
+        "pcm_lr_consistency": ([P, P, I64, I64, D, D, P, P, D, P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

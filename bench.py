@@ -91,6 +91,37 @@ def cloud_bench(H: int = 4000, W: int = 4000) -> dict:
             "note": "host float64 disparity in, host (M,3) points out (PCIe included)"}
 
 
+def stereo_bench(H: int = 4000, W: int = 4000, reps: int = 20) -> dict:
+    """Stereo consistency gathers (row f3) on device-resident H x W inputs, HIP
+    events around `reps` launches: algorithmic bytes = 24 B/px (photo: float64
+    disparity + 2 float32 images + float64 out) and 33 B/px (L/R: 2 float64
+    disparities + float64 out + uint8 mask)."""
+    import torch
+
+    import pcm_amd
+    rng = np.random.default_rng(0)
+    left = torch.from_numpy(rng.uniform(0, 255, (H, W)).astype(np.float32)).cuda()
+    right = torch.from_numpy(rng.uniform(0, 255, (H, W)).astype(np.float32)).cuda()
+    ld = torch.from_numpy(rng.uniform(-150, 60, (H, W))).cuda()
+    rd = -ld + 0.5
+    out = {}
+    for name, fn, bpp in [("photoconsistency", lambda: pcm_amd.photoconsistency_map(left, right, ld, -144), 24),
+                          ("lr_consistency", lambda: pcm_amd.left_right_consistency(ld, rd, -144, threshold=3), 33)]:
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        out[name] = {"ms": ms, "GBps": bpp * H * W / (ms * 1e-3) / 1e9, "bytes_per_px": bpp,
+                     "frac_hbm": bpp * H * W / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    out["pixels"] = H * W
+    return out
+
+
 def pmc_traffic(n, k, d, world):
     """HBM bytes per k_lloyd launch from a rocprofv3 --pmc summary of this same
     workload (tools/evidence.sh; FETCH_SIZE x2 for gfx950's halved wide-read
@@ -123,6 +154,7 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="capture the multi-GPU iteration sequence (incl. the RCCL all-reduce) in a HIP graph")
     ap.add_argument("--no-events", action="store_true", help="calibration: no per-kernel HIP events")
+    ap.add_argument("--stereo", action="store_true", help="also time the stereo consistency gathers (4000x4000)")
     ap.add_argument("--cloud", action="store_true",
                     help="also time the per-pair cloud assembly (4000x4000 disparity) on GPU and CPU")
     args = ap.parse_args()
@@ -295,6 +327,8 @@ def main():
             out["fit"] = fit
         if args.cloud:
             out["cloud_assembly"] = cloud_bench()
+        if args.stereo:
+            out["stereo_gathers"] = stereo_bench()
         if kpp_ms is not None:
             out["kmeanspp_ms"] = kpp_ms   # GPU k-means++ seeding of the same cloud (K centres), host prep included
         if not args.no_cpu and world == 1:

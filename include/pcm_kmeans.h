@@ -201,6 +201,22 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
 int pcm_cloud_assemble(const double *disparity, const uint8_t *validity, int64_t H, int64_t W, double limit,
                        double *points, double *hnorm, int64_t *m_out, double *normal_out, void *stream);
 
+/* ---------------------------------------------------------------- stereo gathers
+ * Per-pixel consistency maps of a rectified pair (H x W, row-major, device):
+ * pcm_photoconsistency replaces members/rafael/disparity/processing.py:94-115
+ * photoconsistency_map (left/right images PCM_F32 or PCM_F64, left_disp
+ * float64 = disparity / 16; out float64 |right[y, rint(x - d)] - left[y, x]| / 255,
+ * 0 where undefined); pcm_lr_consistency replaces disparity.py:229-250
+ * left_right_consistency (out float64 |rd[y, rint(x - d)] + ld[y, x]|, max_disp
+ * where undefined; below (nullable) uint8 = out < threshold, the caller's
+ * `< 3` of disparity.py:170-172; out may be NULL when only the mask is
+ * wanted).  Undefined: d NaN, rint(x - d) outside [0, W), or d < min_disp.
+ * Stream-ordered, no synchronisation. */
+int pcm_photoconsistency(const void *left, const void *right, int img_dtype, const double *left_disp, int64_t H,
+                         int64_t W, double min_disp, double *out, void *stream);
+int pcm_lr_consistency(const double *left_disp, const double *right_disp, int64_t H, int64_t W, double min_disp,
+                       double max_disp, double *out, uint8_t *below, double threshold, void *stream);
+
 /* ---------------------------------------------------------------- dense path
  * Generic-D Lloyd K-means for feature vectors (D <= PCM_DENSE_DMAX, float32 or
  * float64, computed in that precision), replacing one _kmeans_single_lloyd

@@ -65,3 +65,23 @@ def test_gpu_no_validity_and_empty(gpu):
     np.testing.assert_array_equal(pts[:, 1:], ref_pts[:, 1:])
     with pytest.raises(ValueError):
         gpu.assemble_cloud(np.full((8, 8), np.nan))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", [0, 1])
+def test_gpu_matches_reference_block(i):
+    """GPU assembly vs the reference's own plugin.py:147-192 block (golden,
+    tests/golden/make_stereo_golden.py): y, x exact; z, h_norm, normal to 1e-9."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import os
+    import pcm_amd
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "stereo", "cloud.npz"))
+    pts, hn, nrm = pcm_amd.assemble_cloud(g[f"disp{i}"], g[f"valid{i}"])
+    ref = g[f"points{i}"]
+    assert pts.shape == ref.shape
+    np.testing.assert_array_equal(pts[:, 1:], ref[:, 1:])
+    np.testing.assert_allclose(pts[:, 0], ref[:, 0], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(hn, g[f"hnorm{i}"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(nrm, g[f"normal{i}"], rtol=1e-9, atol=1e-12)
