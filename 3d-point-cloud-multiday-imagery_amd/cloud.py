@@ -21,6 +21,13 @@ MAX_DISP = 288   # members/rafael/disparity/constants.py:54-57
 
 def assemble_cloud(disparity, validity=None, max_disp: int = MAX_DISP):
     """Returns (points (M,3) float64 z,y,x, h_norm (M,) float64, normal (3,)) as host arrays."""
+    pts, hn, normal = assemble_cloud_device(disparity, validity, max_disp)
+    return pts.cpu().numpy(), hn.cpu().numpy(), normal
+
+
+def assemble_cloud_device(disparity, validity=None, max_disp: int = MAX_DISP):
+    """As ``assemble_cloud`` but the points and h_norm stay on the device (views of
+    the kernels' outputs): the plugin feeds them to the fused K-means directly."""
     if not torch.cuda.is_available():
         raise _lib.PcmError("assemble_cloud needs a HIP device (no CPU fallback)")
     d = torch.as_tensor(np.asarray(disparity) if not isinstance(disparity, torch.Tensor) else disparity)
@@ -45,4 +52,4 @@ def assemble_cloud(disparity, validity=None, max_disp: int = MAX_DISP):
     M = int(m.value)
     if M == 0:
         raise ValueError("no valid disparity pixels")
-    return pts[:M].cpu().numpy(), hn[:M].cpu().numpy(), normal
+    return pts[:M], hn[:M], normal

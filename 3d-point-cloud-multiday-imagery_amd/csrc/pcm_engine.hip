@@ -749,63 +749,44 @@ int pcm_reloc_candidates(pcm_engine *e, int m, void *records, void *stream) {
     if (!e->fit_ready) return fail(PCM_E_STATE, "no fit in progress");
     hipStream_t s = (hipStream_t)stream;
     const long long n = e->n;
-    if (n == 0) {
-        HIPCHK(hipMemsetAsync(records, 0, (size_t)m * sizeof(RelocRec), s));
-        return 0;
-    }
-    unsigned long long *k1 = nullptr, *k2 = nullptr;
-    uint32_t *v1 = nullptr, *v2 = nullptr;
-    void *tmp = nullptr;
-    size_t tb = 0;
-    int rc = 0;
-    do {
-        hipError_t err;
-        if ((err = hipMalloc(&k1, n * 8)) || (err = hipMalloc(&k2, n * 8)) || (err = hipMalloc(&v1, n * 4)) ||
-            (err = hipMalloc(&v2, n * 4))) {
-            rc = fail(PCM_E_NOMEM, "reloc scratch");
-            break;
-        }
-        // labels of the halted iteration (the iterations keep no label array)
-        if ((rc = launch_labels(e, s, nullptr))) break;
-        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-            using TT = decltype(T);
-            constexpr int D = decltype(DD)::value;
-            return dispatch_l(e, [&](auto L) -> int {
-                using LT = decltype(L);
-                k_reloc_keys<TT, D, LT><<<blocks_for(n), 256, 0, s>>>((const TT *)e->xs, n, e->npad,
-                                                                     (const LT *)e->lab, e->perm, e->C, e->gidx0, k1, v1);
-                LAUNCHCHK();
-                return 0;
-            });
+    HIPCHK(hipMemsetAsync(records, 0, (size_t)m * sizeof(RelocRec), s));
+    if (n == 0) return 0;
+    // keys (8 B/pt) + selection state in the layout's scratch arena (>= 12 B/pt)
+    const size_t need = align_up((size_t)n * 8) + sizeof(RselState);
+    if (ensure(e->ws, e->cap_ws, need) != hipSuccess) return fail(PCM_E_NOMEM, "reloc scratch");
+    unsigned long long *keys = (unsigned long long *)e->ws;
+    RselState *st = (RselState *)((char *)e->ws + align_up((size_t)n * 8));
+    RselState h{};
+    h.prefix = 0ull;
+    h.m_rem = (unsigned long long)std::min<long long>(m, n);
+    HIPCHK(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, s));
+    // labels of the halted iteration (the iterations keep no label array)
+    if (int rc = launch_labels(e, s, nullptr)) return rc;
+    const int hblk = (int)std::min<long long>((n + 255) / 256, (long long)e->num_cu * 4);
+    int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        return dispatch_l(e, [&](auto L) -> int {
+            using LT = decltype(L);
+            k_reloc_keys<TT, D, LT><<<blocks_for(n), 256, 0, s>>>((const TT *)e->xs, n, (const LT *)e->lab, e->perm,
+                                                                 e->C, e->gidx0, keys);
+            LAUNCHCHK();
+            if (m < n)   // exactly the top m; m >= n takes every point (T = 0)
+                for (int pass = 0; pass < 8; ++pass) {
+                    k_rsel_hist<<<hblk, 256, 0, s>>>(keys, n, st, pass);
+                    LAUNCHCHK();
+                    k_rsel_pick<<<1, 64, 0, s>>>(st, pass);
+                    LAUNCHCHK();
+                }
+            k_reloc_gather<TT, D, LT><<<blocks_for(n), 256, 0, s>>>(keys, n, (const TT *)e->xs, (const LT *)e->lab,
+                                                                   e->qe, st, m, (RelocRec *)records);
+            LAUNCHCHK();
+            return 0;
         });
-        if (rc) break;
-        if ((err = rocprim::radix_sort_pairs_desc(nullptr, tb, k1, k2, v1, v2, (size_t)n, 0u, 64u, s)) ||
-            (err = hipMalloc(&tmp, tb))) {
-            rc = fail(PCM_E_HIP, "reloc sort setup");
-            break;
-        }
-        if ((err = rocprim::radix_sort_pairs_desc(tmp, tb, k1, k2, v1, v2, (size_t)n, 0u, 64u, s))) {
-            rc = fail(PCM_E_HIP, "reloc sort");
-            break;
-        }
-        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-            using TT = decltype(T);
-            constexpr int D = decltype(DD)::value;
-            return dispatch_l(e, [&](auto L) -> int {
-                using LT = decltype(L);
-                k_reloc_gather<TT, D, LT><<<blocks_for(m), 256, 0, s>>>(k2, v2, m, n, (const TT *)e->xs, e->npad,
-                                                                       (const LT *)e->lab, e->qe, (RelocRec *)records);
-                LAUNCHCHK();
-                return 0;
-            });
-        });
-        if (rc) break;
-        if ((err = hipStreamSynchronize(s))) { rc = fail(PCM_E_HIP, "reloc sync"); break; }
-    } while (0);
-    void *ps[] = {k1, k2, v1, v2, tmp};
-    for (void *p : ps)
-        if (p) (void)hipFree(p);
-    return rc;
+    });
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
 }
 
 int pcm_reloc_apply(pcm_engine *e, const void *records, int n_rec, void *stream) {

@@ -1477,12 +1477,18 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
 }
 
 // ------------------------------------------------------------------ relocation
-// key = dist_bits << 32 | (0xffffffff - global index); sort descending.
+// This rank's m farthest points from their centre (_k_means_common.pyx:185-187)
+// by an exact radix SELECT over unique 64-bit keys (no sort, no N-sized
+// allocation: the keys live in the layout's scratch arena):
+//   key = dist_bits << 32 | (0xffffffff - global index)   (distance desc, row asc)
+// 8 passes pick the m-th largest key T one byte at a time (MSB first); then
+// every point with key >= T writes its record (any order: k_reloc_apply ranks
+// the records it receives).
 template <typename T, int D, typename LT>
-__global__ __launch_bounds__(256) void k_reloc_keys(const T *__restrict__ xs, long long n, long long npad,
+__global__ __launch_bounds__(256) void k_reloc_keys(const T *__restrict__ xs, long long n,
                                                     const LT *__restrict__ lab, const uint32_t *__restrict__ perm,
                                                     const float4 *__restrict__ C, long long gidx0,
-                                                    unsigned long long *__restrict__ keys, uint32_t *__restrict__ vals) {
+                                                    unsigned long long *__restrict__ keys) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= n) return;
     float x[D];
@@ -1490,7 +1496,45 @@ __global__ __launch_bounds__(256) void k_reloc_keys(const T *__restrict__ xs, lo
     float d = dist_canon<D>(x, C[(int)lab[i]]);
     unsigned long long g = (unsigned long long)(gidx0 + perm[i]);
     keys[i] = ((unsigned long long)__float_as_uint(d) << 32) | (0xffffffffull - (g & 0xffffffffull));
-    vals[i] = (uint32_t)i;
+}
+
+struct RselState {
+    unsigned long long prefix;    // selected high bytes of T
+    unsigned long long m_rem;     // how many of the keys matching `prefix` still belong to the top m
+    unsigned int hist[256];
+    unsigned int count_out;
+    unsigned int pad;
+};
+
+// Histogram of byte `pass` (0 = most significant) of the keys whose higher bytes equal the prefix.
+__global__ __launch_bounds__(256) void k_rsel_hist(const unsigned long long *__restrict__ keys, long long n,
+                                                   RselState *__restrict__ st, int pass) {
+    __shared__ unsigned int h[256];
+    h[threadIdx.x] = 0u;
+    __syncthreads();
+    const int shift = 56 - 8 * pass;
+    const unsigned long long hmask = pass ? (~0ull << (64 - 8 * pass)) : 0ull;
+    const unsigned long long prefix = st->prefix;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const unsigned long long k = keys[i];
+        if ((k & hmask) == prefix) atomicAdd(&h[(k >> shift) & 0xffu], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&st->hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// One thread: the byte value holding the m_rem-th largest matching key.
+__global__ void k_rsel_pick(RselState *__restrict__ st, int pass) {
+    if (threadIdx.x != 0) return;
+    unsigned long long above = 0ull;
+    int v = 255;
+    for (; v > 0; --v) {
+        if (above + st->hist[v] >= st->m_rem) break;
+        above += st->hist[v];
+    }
+    st->prefix |= (unsigned long long)v << (56 - 8 * pass);
+    st->m_rem -= above;
+    for (int b = 0; b < 256; ++b) st->hist[b] = 0u;
 }
 
 struct RelocRec {
@@ -1500,23 +1544,24 @@ struct RelocRec {
     int32_t xq[4];
 };
 
+// Every point with key >= T (the top m; keys are unique) writes its record.
 template <typename T, int D, typename LT>
-__global__ void k_reloc_gather(const unsigned long long *__restrict__ keys, const uint32_t *__restrict__ vals, int m,
-                               long long n, const T *__restrict__ xs, long long npad, const LT *__restrict__ lab,
-                               QExp qe, RelocRec *__restrict__ out) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= m) return;
+__global__ __launch_bounds__(256) void k_reloc_gather(const unsigned long long *__restrict__ keys, long long n,
+                                                      const T *__restrict__ xs, const LT *__restrict__ lab, QExp qe,
+                                                      RselState *__restrict__ st, int m, RelocRec *__restrict__ out) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = keys[i];
+    if (k < st->prefix) return;
+    const unsigned int slot = atomicAdd(&st->count_out, 1u);
+    if (slot >= (unsigned)m) return;   // cannot happen (exactly min(m, n) keys >= T)
     RelocRec r;
-    r.key = 0ull; r.label = 0; r.valid = 0;
+    r.key = k;
+    r.label = (int)lab[i];
+    r.valid = 1;
     r.xq[0] = r.xq[1] = r.xq[2] = r.xq[3] = 0;
-    if (t < n) {
-        uint32_t i = vals[t];
-        r.key = keys[t];
-        r.label = (int)lab[i];
-        r.valid = 1;
-        for (int a = 0; a < D; ++a) r.xq[a] = fixed_i(to_f<T>(xs[xs_index<D>(i, a)]), qe.q[a]);
-    }
-    out[t] = r;
+    for (int a = 0; a < D; ++a) r.xq[a] = fixed_i(to_f<T>(xs[xs_index<D>(i, a)]), qe.q[a]);
+    out[slot] = r;
 }
 
 // Single block: global top-n_empty over all ranks' records, moves applied to

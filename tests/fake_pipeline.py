@@ -55,3 +55,29 @@ class SyntheticPairExtractor:
                                     "properties": {"height": h_norm}, "scale": (1, 1, 1), "opacity": 0.8,
                                     "face_colormap": "turbo", "face_color": "height"}, "points"))
         return layers
+
+
+class SyntheticStages:
+    """Stand-in for pcm_amd.pipeline.ReferenceStereoStages: per-pair products
+    (disparity, validity mask, photoconsistency, debug image layers) of the
+    shape the reference's disparity_map returns (disparity.py:21-226)."""
+
+    def __init__(self, n_pairs=2, shape=(120, 160), seed=0, fail_at=None):
+        self.n_pairs, self.shape, self.seed, self.fail_at = n_pairs, shape, seed, fail_at
+
+    def pairs(self, kml_path, is_debug_mode=True, is_debug_pair=False, is_one_random_pair=True, n=10):
+        from pcm_amd.pipeline import PairProducts
+        rng = np.random.default_rng(self.seed)
+        H, W = self.shape
+        yy, xx = np.mgrid[0:H, 0:W]
+        for p in range(min(self.n_pairs, n)):
+            if self.fail_at == p:
+                raise RuntimeError("synthetic stereo failure")
+            disparity = -16.0 * (8 * np.sin(xx / 23.0 + p) + 5 * np.cos(yy / 17.0) + rng.normal(0, 0.3, (H, W)))
+            disparity[rng.random((H, W)) < 0.02] = 16.0 * 1000           # WLS sentinel
+            validity = rng.random((H, W)) > 0.1
+            photo = np.where(rng.random((H, W)) < 0.8, rng.uniform(0, 0.3, (H, W)), 0.0)
+            image_layers = [(rng.random((H, W)), {"name": f"{PREFIX} Input Left", "colormap": "gray"}, "image")] \
+                if is_debug_mode else []
+            yield PairProducts(disparity=disparity, validity=validity, photoconsistency=photo,
+                               image_layers=image_layers)

@@ -246,3 +246,17 @@ def test_unpruned_full_lists(pcm):
     ref = R.lloyd_fit(X, C0, max_iter=25, tol=0.0, fast=True)
     res = gpu_fit(pcm, X, C0, 25)
     assert_same(res, ref, "unpruned")
+
+
+def test_relocation_distance_ties_topm(pcm):
+    """Radix-select relocation: many points at exactly the same (largest)
+    distance -> the lowest global rows move first (distance desc, row asc)."""
+    X = R.splitmix_uniform(200_000, 3, 33)
+    far = np.array([7.0, 7.0, 7.0], np.float32)
+    X[5_000:5_400] = far                       # 400 identical far points (equal keys' distance bits)
+    X[150_000:150_200] = far
+    C0 = np.concatenate([X[:40], np.full((12, 3), 900.0, np.float32) + np.arange(12, dtype=np.float32)[:, None]])
+    ref = R.lloyd_fit(X, C0, max_iter=12, fast=True)
+    res = gpu_fit(pcm, X, C0, 12, chunk=2)
+    assert res.relocations >= 1
+    assert_same(res, ref, "reloc ties")

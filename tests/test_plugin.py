@@ -76,3 +76,69 @@ def test_gpu_path_fails_loudly_without_device():
     plugin = pcm_amd.HeightMapExtractor(base=SyntheticPairExtractor(n_pairs=1, shape=(40, 40)), n_clusters=4)
     out = plugin.run("roi.kml")
     assert out[0][1]["name"].startswith("Error:")
+
+
+# ---------------------------------------------------------------- GPU-stages path (rows a1-a4 / f2 / f4)
+def oracle_assemble(disparity, validity):
+    from oracle import cloud_ref
+    pts, hn, _ = cloud_ref.assemble(disparity, validity)
+    return pts, hn
+
+
+def test_stages_path_layers_and_fusion_cpu(tmp_path):
+    from fake_pipeline import SyntheticStages
+    stages = SyntheticStages(n_pairs=2, shape=(70, 90))
+    out = tmp_path / "fused.npz"
+    plugin = pcm_amd.HeightMapExtractor(stages=stages, n_clusters=12, fit=oracle_fit, _assemble=oracle_assemble,
+                                        export_path=str(out))
+    layers = plugin.run("roi.kml")
+    names = [l[1]["name"].replace("[Multi-day 3D Point Cloud] ", "") for l in layers]
+    per_pair = ["Input Left", "Disparity", "Photoconsistency", "Invalid Mask", "3D Point Cloud"]   # plugin.py:119-233
+    assert names == per_pair * 2 + ["Fused K-means Centroids", "Fused 3D Point Cloud"]
+    clouds = [l[0] for l in layers if l[2] == "points" and l[1]["name"].endswith("] 3D Point Cloud")]
+    X = np.concatenate(clouds).astype(np.float32)
+    ref = R.lloyd_fit(X, X[R.init_indices(X.shape[0], 12)], max_iter=300,
+                      tol=float(np.mean(np.var(X.astype(np.float64), axis=0)) * 1e-4))
+    np.testing.assert_array_equal(layers[-1][1]["properties"]["cluster"], ref["labels"])
+    # the Disparity image holds h_norm at the valid pixels (normalise_for_display of the relative heights)
+    disp_img, pts, hn = layers[1][0], layers[4][0], layers[4][1]["properties"]["height"]
+    np.testing.assert_array_equal(disp_img[pts[:, 1].astype(int), pts[:, 2].astype(int)], hn)
+    assert np.isnan(disp_img).sum() == disp_img.size - pts.shape[0]
+    # f4: the on-disk fused cloud
+    f = pcm_amd.plugin.load_fused(str(out))
+    np.testing.assert_array_equal(f["cluster"], ref["labels"])
+    np.testing.assert_array_equal(f["points"], X.astype(np.float64))
+    assert f["centers"].shape == (12, 3) and int(f["counts"].sum()) == X.shape[0]
+
+
+def test_stages_error_becomes_error_layer():
+    from fake_pipeline import SyntheticStages
+    plugin = pcm_amd.HeightMapExtractor(stages=SyntheticStages(fail_at=1), fit=oracle_fit, _assemble=oracle_assemble)
+    out = plugin.run("roi.kml")
+    assert len(out) == 1 and out[0][1]["name"] == "Error: synthetic stereo failure"
+
+
+@pytest.mark.gpu
+def test_gpu_stages_path_device_fusion():
+    """GPU cloud assembly on the plugin path (no host round trip into the K-means):
+    the fused labels equal an oracle fit of the assembled clouds the layers show."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from fake_pipeline import SyntheticStages
+    plugin = pcm_amd.HeightMapExtractor(stages=SyntheticStages(n_pairs=3, shape=(120, 150)), n_clusters=64,
+                                        max_iter=40, tol=0.0)
+    layers = plugin.run("roi.kml")
+    assert layers[-1][1]["name"].endswith("Fused 3D Point Cloud"), layers[0][1]["name"]
+    clouds = [l[0] for l in layers if l[2] == "points" and l[1]["name"].endswith("] 3D Point Cloud")]
+    X = np.concatenate(clouds).astype(np.float32)
+    ref = R.lloyd_fit(X, X[R.init_indices(X.shape[0], 64)], max_iter=40, fast=True)
+    np.testing.assert_array_equal(layers[-1][1]["properties"]["cluster"], ref["labels"])
+    np.testing.assert_array_equal(layers[-2][0].astype(np.float32), ref["centers"])
+    # each pair's cloud is the GPU assembly of that pair (= the oracle to float64 rounding)
+    from oracle import cloud_ref
+    st = SyntheticStages(n_pairs=3, shape=(120, 150))
+    for pp, cl in zip(st.pairs("roi.kml"), clouds):
+        ref_pts, _, _ = cloud_ref.assemble(pp.disparity, pp.validity)
+        np.testing.assert_array_equal(cl[:, 1:], ref_pts[:, 1:])
+        np.testing.assert_allclose(cl[:, 0], ref_pts[:, 0], rtol=1e-9, atol=1e-9)
