@@ -95,7 +95,8 @@ int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream,
                     double *lo, double *hi, double *maxabs);
 
 /* Layout, step 2 (host-synchronising, once): bin rows into the pruning grid,
- * sort them into cell-contiguous SoA order and build the tile list.  `q` are the
+ * sort them into cell order (AoSoA-4: groups of 4 points stored coordinate-major)
+ * and build the tile list.  `q` are the
  * GLOBAL fixed-point exponents (identical on every rank), `gidx0` the global row
  * index of local row 0 (relocation tie-break).  X must stay unchanged until
  * this call returns. */
