@@ -86,27 +86,62 @@ def prepare(engine, X, group=None):
     return q, n_total
 
 
-def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False):
+def _uses_graph(graph, world, group, split):
+    import torch.distributed as dist
+    if graph is not None:
+        return bool(graph)
+    if not (world > 1 or split) or not dist.is_initialized():
+        return False
+    try:
+        return dist.get_backend(group) == "nccl"   # RCCL collectives can be captured; gloo's cannot
+    except Exception:   # noqa: BLE001
+        return False
+
+
+def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, graph=None):
     """Iteration phase on a prepared engine.  Returns (status, relocations).
 
     One process: ``pcm_iterate`` (k_lloyd + fused k_step per iteration).  Several
-    (or ``split``): ``iter_local`` (k_lloyd + k_fold) -> all-reduce of the
-    statistics (only when world > 1) -> ``iter_global`` (k_step on them)."""
+    (or ``split``): ``iter_local`` (k_lloyd accumulating into the statistics
+    buffer) -> all-reduce of the statistics (only when world > 1) ->
+    ``iter_global`` (k_step on them).  With RCCL (``graph`` None = auto) a chunk
+    of that sequence is captured once in a HIP graph and replayed: no host launch
+    gaps between the kernels and the collective; the device control block gates
+    iterations queued past convergence or a halt either way."""
+    import torch
     import torch.distributed as dist
     world, _ = _world(group)
     engine.begin(C0, tol, max_iter)
     relocs = 0
     it = 0
+    use_graph = _uses_graph(graph, world, group, split)
+    captured = None
+
+    def seq(n):
+        for _ in range(n):
+            engine.iter_local()
+            if world > 1:
+                dist.all_reduce(engine.stats, group=group)
+            engine.iter_global()
+
     while True:
         n_enq = max(1, min(chunk, max_iter - it))
         if world == 1 and not split:
             engine.iterate(n_enq)
+        elif use_graph and n_enq == chunk:
+            if captured is None:
+                try:
+                    captured = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(captured):
+                        seq(chunk)
+                except Exception:   # noqa: BLE001 -- capture refused: eager launches
+                    captured, use_graph = None, False
+                    torch.cuda.synchronize()
+                    seq(n_enq)
+            if captured is not None:
+                captured.replay()
         else:
-            for _ in range(n_enq):
-                engine.iter_local()
-                if world > 1:
-                    dist.all_reduce(engine.stats, group=group)
-                engine.iter_global()
+            seq(n_enq)
         st = engine.status()
         if st["halt"]:
             recs = engine.reloc_candidates(int(st["n_empty"]))
@@ -138,7 +173,7 @@ def finish(engine, group=None):
 
 
 def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=None, chunk: int = 8,
-              engine=None, split: bool = False) -> LloydResult:
+              engine=None, split: bool = False, graph=None) -> LloydResult:
     """Fit K-means (Lloyd) to this rank's shard ``X`` (N_local, D) from ``centers_init`` (K, D).
 
     ``tol`` is the absolute centre-shift tolerance (sklearn's ``_tolerance``
@@ -151,7 +186,7 @@ def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=N
         from .engine import Engine
         engine = Engine(X.shape[1], centers_init.shape[0], X.dtype, max_iter=max_iter)
     prepare(engine, X, group)
-    st, relocs = run(engine, centers_init, max_iter, tol, group, chunk, split)
+    st, relocs = run(engine, centers_init, max_iter, tol, group, chunk, split, graph)
     labels, centers, inertia = finish(engine, group)
     ch, sh = engine.history(int(st["iter"]))
     return LloydResult(labels=labels, centers=centers, inertia=inertia, n_iter=int(st["iter"]),

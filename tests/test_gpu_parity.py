@@ -260,3 +260,29 @@ def test_relocation_distance_ties_topm(pcm):
     res = gpu_fit(pcm, X, C0, 12, chunk=2)
     assert res.relocations >= 1
     assert_same(res, ref, "reloc ties")
+
+
+@pytest.mark.parametrize("name", ["cfg1_n10k_k8", "empty_reloc"])
+def test_split_sequence_graph_replay(pcm, name):
+    """The multi-GPU call sequence captured in a HIP graph (a 1-rank RCCL group:
+    k_lloyd -> all_reduce -> k_step per iteration, replayed per chunk) gives the
+    oracle's fit, relocation included."""
+    import socket
+    import torch.distributed as dist
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    X, C0 = g["X"], g["C0"]
+    ref = R.lloyd_fit(X, C0, max_iter=300, tol=0.0, fast=True)
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0,
+                            device_id=torch.device("cuda", 0))
+    try:
+        res = pcm.lloyd_fit(torch.from_numpy(np.ascontiguousarray(X)).cuda(),
+                            torch.from_numpy(np.ascontiguousarray(C0, dtype=np.float32)).cuda(), max_iter=300,
+                            tol=0.0, chunk=4, split=True, graph=True)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    assert_same(res, ref, name + " graph")
