@@ -240,7 +240,9 @@ void make_grid(Grid &g, int d, const double *lo, const double *hi, double target
 // points per cell: fewer, fuller tiles (a tile round is 1024 points) outweigh
 // the slightly longer candidate lists (swept on 12.5M / 100M clouds).
 void choose_grid(pcm_engine *e) {
-    double target = std::min(32.0 * e->k, (double)e->n / 2800.0);
+    // D = 4: smaller cells (~1k points) shorten the lists more than the tiles
+    // cost (config-5 shape: 20736 -> 65536 cells, 913 -> 846 us per iteration)
+    double target = std::min(32.0 * e->k, (double)e->n / (e->d >= 4 ? 1000.0 : 2800.0));
     if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     make_grid(e->g, e->d, e->lo, e->hi, target);
     if (e->k <= 1) e->g.prune = 0;
@@ -530,10 +532,12 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
 
 // Candidate blocks per coarse cell: enough blocks to fill the chip on small
 // (sharded) clouds; D = 4 coarse cells hold 256 fine cells.
+// Measured (tools/r2_sweep.sh): 12.5M-point shard (64 coarse cells) 8 -> 39 us
+// vs 4 -> 47 us per update; 100M (512 coarse cells) 1; D = 4, K = 4096: 32.
 static int cand_bpc(const pcm_engine *e) {
     if (const char *ov = std::getenv("PCM_CAND_BPC_RT")) return std::max(1, std::atoi(ov));   // tuning sweeps only
-    if (e->d >= 4) return 16;
-    long long b = ((long long)e->num_cu + e->g.ncoarse - 1) / std::max(1LL, e->g.ncoarse);
+    if (e->d >= 4) return 32;
+    long long b = (2LL * e->num_cu + e->g.ncoarse - 1) / std::max(1LL, e->g.ncoarse);
     return (int)std::max(1LL, std::min(8LL, b));
 }
 
@@ -665,10 +669,18 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
 // (multi-GPU / resume) or nullptr (single GPU: partials[parity]).  K <=
 // KSTEP_MAX: one fused k_step launch; otherwise k_global then k_cand.  The
 // relocation resume always takes k_global (it handles `resume`) + k_cand.
+static int kstep_max() {
+    static const int v = [] {
+        const char *ov = std::getenv("PCM_KSTEP_MAX");   // tuning sweeps only
+        return ov ? std::min(KSTEP_MAX, std::atoi(ov)) : KSTEP_MAX;
+    }();
+    return v;
+}
+
 static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bool resume_path) {
     int rc = dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        if (e->k <= KSTEP_MAX && !resume_path) {
+        if (e->k <= kstep_max() && !resume_path) {
             const int bpc = cand_bpc(e);
             const size_t lds = (size_t)e->k * sizeof(float4);
             static bool attr_set[MAXD + 1] = {false, false, false, false, false};

@@ -29,7 +29,9 @@ constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-
 #endif
 constexpr int TPB = PCM_TPB;       // assign block size
 constexpr int TILE = 32 * TPB;     // max points per tile: <= 32 per lane, 64 per shared LDS word (see AccL)
-constexpr int KSTEP_MAX = 4096;    // k_step keeps the K new centres in LDS (<= 64 KB of gfx950's 160 KB)
+// k_step keeps the K new centres in LDS; above 2048 (32 KB) its occupancy drops
+// to 2 blocks/CU and k_global + k_cand is faster (K = 4096, D = 4: 241 vs 439 us)
+constexpr int KSTEP_MAX = 2048;
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int QBITS = 25;
 // Pruning margins (see DESIGN.md "Exactness of pruning").
@@ -555,7 +557,10 @@ __global__ __launch_bounds__(CAND_TPB) void k_cand(Grid g, const float4 *__restr
     float4 *ref = cref + (size_t)ctrl->ref_sel * K;
     for (long long j = blockIdx.x * (long long)CAND_TPB + threadIdx.x; j < K; j += (long long)gridDim.x * CAND_TPB)
         ref[j] = C[j];
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->budget = 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctrl->budget = 0.0;
+        if (gate) ctrl->rebuilds += 1u;   // per-iteration lists (K > KSTEP_MAX, resume)
+    }
     cand_body<D>(g, C, K, fc_cnt, fc_rec, fc_lab, bpc);
 }
 
@@ -892,6 +897,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LSLOT+1)*(D+1)][TPB]
     __shared__ float4 crec[2][CAPF];
     __shared__ int32_t cid[2][CAPF];
+    // list positions LSLOT .. CAPF-1 of long (non-FULL) lists: block-shared int64
+    // words (ds_add_u64), folded at the tile boundary like the slots.  D = 4 only
+    // (long lists are the norm there); at D <= 3 the 1.5 KB would cost a
+    // resident block per CU, and the rare long list uses global int64 atomics.
+    constexpr bool kOvf = D >= 4;
+    __shared__ unsigned long long ovf[kOvf ? (CAPF - LSLOT) * (D + 1) : 1];
     const int tid = threadIdx.x;
     const unsigned G = gridDim.x;
     const unsigned nt = *A.ntiles;
@@ -907,6 +918,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     };
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     for (int e = tid; e < AccL<D>::words; e += TPB) acc[e] = 0u;
+    if (kOvf)
+        for (int e = tid; e < (CAPF - LSLOT) * (D + 1); e += TPB) ovf[e] = 0ull;
     uint32_t *const myacc = acc + (tid & (AW - 1));
 
     // Candidate list of tile hh into LDS half sp: scalar loads, 4 records per
@@ -1011,8 +1024,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
             for (int e = 0; e < 4; ++e) {
                 const bool v = whole || ((i0 + e >= h.start) && (i0 + e < h.end));
                 if (!(v && bj[e] >= LSLOT)) continue;
-                const int lbl = h.full ? bj[e] : cid[par][bj[e]];
-                unsigned long long *pp = prep + (size_t)lbl * (D + 1);
+                // non-FULL: the block's LDS int64 words; FULL (all K): global int64
+                unsigned long long *pp = (h.full || !kOvf) ? prep + (size_t)(h.full ? bj[e] : cid[par][bj[e]]) * (D + 1)
+                                                           : ovf + (size_t)(bj[e] - LSLOT) * (D + 1);
                 for (int a = 0; a < D; ++a)
                     atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
                 atomicAdd(pp + D, 1ull);
@@ -1053,6 +1067,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
                     atomicAdd(prep + (size_t)cid[par][slot] * (D + 1) + qq, (unsigned long long)sacc);
                 }
             }
+            if (kOvf && !h.full && h.mm > LSLOT)
+                for (int i = tid; i < (h.mm - LSLOT) * (D + 1); i += TPB) {
+                    const unsigned long long w = ovf[i];
+                    if (w) {
+                        atomicAdd(prep + (size_t)cid[par][LSLOT + i / (D + 1)] * (D + 1) + i % (D + 1), w);
+                        ovf[i] = 0ull;
+                    }
+                }
         }
         if (t + G >= nt) return false;
         install(h1, par ^ 1);

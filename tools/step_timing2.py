@@ -1,6 +1,6 @@
 """Calibration (debug build -DPCM_DBG_TIMING): per-block phase times of the
-fused k_step of the last of `iters` iterations (config 3).  usage:
-python tools/step_timing2.py SO_PATH [iters]"""
+fused k_step of the last of `iters` iterations.  usage:
+python tools/step_timing2.py SO_PATH [iters] [N K D]  (default config 3)"""
 import ctypes, os, sys
 import numpy as np
 os.environ["PCM_SO"] = sys.argv[1]
@@ -8,7 +8,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pcm_amd import lloyd, _lib
 from pcm_amd.engine import Engine, synth_rows, synth_uniform
-N, K, D = 100_000_000, 1024, 3
+N, K, D = (int(v) for v in sys.argv[3:6]) if len(sys.argv) > 5 else (100_000_000, 1024, 3)
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 X = synth_uniform(N, D, seed=0, start=0)
 C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0)
@@ -34,6 +34,12 @@ print("centres+drift us (start->6): p50 %.1f max %.1f" % (us(np.median(w[:, 6] -
 print("body us (6->3): p50 %.1f max %.1f" % (us(np.median(w[:, 3] - w[:, 6])), us((w[:, 3] - w[:, 6]).max())))
 b = t[-1]
 print("b0: centres %.1f, bookkeeping %.1f us" % (us(b[6] - b[0]), us(b[3] - b[6])))
+c = t[:-1]
+for k0, k1, name in ((6, 4, "coarse reference"), (4, 5, "coarse prune"), (5, 1, "coarse compact"), (1, 2, "children")):
+    ok = (c[:, k0] > 0) & (c[:, k1] > 0)
+    if ok.any():
+        dd = c[ok, k1] - c[ok, k0]
+        print("%s us: p50 %.1f max %.1f" % (name, us(np.median(dd)), us(dd.max())))
 print("end of bodies (rel. first start) us: p50 %.1f max %.1f" % (us(np.median(t[:, 3] - t0)), us(t[:, 3].max() - t0)))
 last = t[:, 7].max()
 print("last block finished at %.1f us" % us(last - t0))
