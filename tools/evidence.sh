@@ -10,9 +10,9 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $T/smoke.
 tail -1 $T/smoke.txt
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 for P in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $T/pmc_$P -o run -- python3 bench.py --no-cpu --steps 5 --warmup 3 > $T/pmc_$P.log 2>&1 || { echo "FAIL pmc $P"; tail -5 $T/pmc_$P.log; exit 1; }
+  timeout -k 10 -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $T/pmc_$P -o run -- python3 bench.py --no-cpu --no-graph --fit-iters 0 --steps 5 --warmup 3 > $T/pmc_$P.log 2>&1 || { echo "FAIL pmc $P"; tail -5 $T/pmc_$P.log; exit 1; }
 done
 python tools/pmc_summary.py k_lloyd $T/pmc_FETCH_SIZE $T/pmc_WRITE_SIZE > $T/pmc_k_lloyd.json && cat $T/pmc_k_lloyd.json
-bash tools/prof.sh $T/prof --steps 20 --warmup 3 | tail -8 || exit 1
-PCM_PMC_JSON=$T/pmc_k_lloyd.json timeout -k 10 400 python bench.py --fit --cloud > $T/bench.txt 2>&1 || { tail -20 $T/bench.txt; exit 1; }
+bash tools/prof.sh $T/prof --steps 20 --warmup 3 --fit | tail -14 || exit 1
+PCM_PMC_JSON=$T/pmc_k_lloyd.json timeout -k 10 400 python bench.py --fit --cloud --stereo > $T/bench.txt 2>&1 || { tail -20 $T/bench.txt; exit 1; }
 tail -1 $T/bench.txt
