@@ -562,6 +562,11 @@ static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
     return (int)std::max(1LL, std::min<long long>(e->ntiles_cap, (long long)per_cu * e->num_cu));
 }
 
+static int lloyd_slots(const pcm_engine *e) {
+    if (const char *ov = std::getenv("PCM_LSLOT_RT")) return std::atoi(ov) == 8 ? 8 : LSLOT;   // tuning sweeps only
+    return (e->g.prune && e->g.ncells >= 8LL * e->k) ? 8 : LSLOT;
+}
+
 static LloydArgs lloyd_args(pcm_engine *e) {
     LloydArgs A{};
     A.xs = e->xs;
@@ -650,9 +655,17 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
         if (e->n > 0) {
-            const size_t lds = (size_t)AccL<D>::words * sizeof(uint32_t);
-            k_lloyd<TT, D><<<assign_grid(e, (const void *)k_lloyd<TT, D>, lds), TPB, lds, s>>>(A, e->tiles, e->fc_rec,
-                                                                                              e->fc_lab, e->C, e->fc_cnt);
+            // lane slots per thread: 8 on fine grids (>= 8 cells per centre: lists
+            // of ~3 at config 3; 13.5 KB of LDS -> 5 waves/SIMD, 247 -> 237 us),
+            // else 16 (12.5M-point shard: lists of ~6, 53 vs 57 us)
+            auto launch = [&](auto LSc) {
+                constexpr int LS = decltype(LSc)::value;
+                const size_t lds = (size_t)AccL<D, LS>::words * sizeof(uint32_t);
+                k_lloyd<TT, D, LS><<<assign_grid(e, (const void *)k_lloyd<TT, D, LS>, lds), TPB, lds, s>>>(
+                    A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
+            };
+            if (D <= 3 && lloyd_slots(e) == 8) launch(std::integral_constant<int, 8>{});
+            else launch(std::integral_constant<int, LSLOT>{});
             LAUNCHCHK();
         }
         return timing_mark(e, 2, s);

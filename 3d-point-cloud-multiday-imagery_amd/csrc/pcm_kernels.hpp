@@ -718,8 +718,8 @@ constexpr int LSLOT = PCM_LSLOT;
 // banks per half-wave whatever the slots.  A word sums <= 2 x 32 points of
 // |xq| < 2^25 per tile: < 2^31, exact in int32.
 constexpr int AW = TPB >= 128 ? TPB / 2 : TPB;   // one wave per block: no sharing (same-instruction lanes must not collide)
-template <int D> struct AccL {
-    static constexpr int rows = (LSLOT + 1) * (D + 1);   // + junk slot
+template <int D, int LS = LSLOT> struct AccL {
+    static constexpr int rows = (LS + 1) * (D + 1);   // + junk slot
     static constexpr int words = AW * rows;
 };
 
@@ -887,22 +887,28 @@ __device__ __forceinline__ void scan4_s(const float4 *__restrict__ C, int mm, co
 #ifndef PCM_WPE
 #define PCM_WPE 4
 #endif
-template <typename T, int D>
+template <typename T, int D, int LS>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8))) void k_lloyd(LloydArgs A, const uint4 *__restrict__ tiles,
                                                const float4 *__restrict__ fc_rec,
                                                const int32_t *__restrict__ fc_lab,
                                                const float4 *__restrict__ Call,
                                                const uint32_t *__restrict__ fc_cnt) {
     if (gated(A.ctrl)) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LSLOT+1)*(D+1)][TPB]
+    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LS+1)*(D+1)][TPB]
     __shared__ float4 crec[2][CAPF];
     __shared__ int32_t cid[2][CAPF];
-    // list positions LSLOT .. CAPF-1 of long (non-FULL) lists: block-shared int64
-    // words (ds_add_u64), folded at the tile boundary like the slots.  D = 4 only
-    // (long lists are the norm there); at D <= 3 the 1.5 KB would cost a
-    // resident block per CU, and the rare long list uses global int64 atomics.
-    constexpr bool kOvf = D >= 4;
-    __shared__ unsigned long long ovf[kOvf ? (CAPF - LSLOT) * (D + 1) : 1];
+    // list positions LS .. CAPF-1 of long (non-FULL) lists: block-shared int64
+    // words (ds_add_u64), folded at the tile boundary like the slots.  Used by
+    // the 8-slot variant (fine grids, short lists: the smaller LDS footprint
+    // gives 5 waves/SIMD) and at D = 4 (long lists are the norm there); the
+    // 16-slot D <= 3 variant leaves them out (1.5 KB would cost a resident
+    // block per CU) and sends the rare long list to global int64 atomics.
+#ifdef PCM_OVF_ALL
+    constexpr bool kOvf = true;
+#else
+    constexpr bool kOvf = D >= 4 || LS < LSLOT;
+#endif
+    __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
     const int tid = threadIdx.x;
     const unsigned G = gridDim.x;
     const unsigned nt = *A.ntiles;
@@ -917,16 +923,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         return v;
     };
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
-    for (int e = tid; e < AccL<D>::words; e += TPB) acc[e] = 0u;
+    for (int e = tid; e < AccL<D, LS>::words; e += TPB) acc[e] = 0u;
     if (kOvf)
-        for (int e = tid; e < (CAPF - LSLOT) * (D + 1); e += TPB) ovf[e] = 0ull;
+        for (int e = tid; e < (CAPF - LS) * (D + 1); e += TPB) ovf[e] = 0ull;
     uint32_t *const myacc = acc + (tid & (AW - 1));
 
     // Candidate list of tile hh into LDS half sp: scalar loads, 4 records per
     // chunk, written by lanes 0-3 (uniform cell -> SMEM, no vector loads).
     auto install = [&](const TileL &hh, int sp) {
         if (hh.full) {
-            if (tid < LSLOT) cid[sp][tid] = tid;
+            if (tid < LS) cid[sp][tid] = tid;
             return;
         }
         const float4 *pr = lrec + (size_t)hh.cell * CAPF;
@@ -1006,9 +1012,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         bool over = false;
         for (int e = 0; e < 4; ++e) {
             const bool v = whole || ((i0 + e >= h.start) && (i0 + e < h.end));
-            const bool hi = bj[e] >= LSLOT;
+            const bool hi = bj[e] >= LS;
             over |= v && hi;
-            sl[e] = (v && !hi) ? bj[e] : LSLOT;
+            sl[e] = (v && !hi) ? bj[e] : LS;
         }
 #ifdef PCM_ABL_NOACC
         for (int e = 0; e < 4; ++e) sl[e] = (int)(x[e][0] * x[e][1] * x[e][2]) & 1;
@@ -1020,13 +1026,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
             for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
             atomicAdd(ap + D * AW, 1u);
         }
-        if (over) {   // list positions >= LSLOT (long lists only)
+        if (over) {   // list positions >= LS (long lists only)
             for (int e = 0; e < 4; ++e) {
                 const bool v = whole || ((i0 + e >= h.start) && (i0 + e < h.end));
-                if (!(v && bj[e] >= LSLOT)) continue;
+                if (!(v && bj[e] >= LS)) continue;
                 // non-FULL: the block's LDS int64 words; FULL (all K): global int64
                 unsigned long long *pp = (h.full || !kOvf) ? prep + (size_t)(h.full ? bj[e] : cid[par][bj[e]]) * (D + 1)
-                                                           : ovf + (size_t)(bj[e] - LSLOT) * (D + 1);
+                                                           : ovf + (size_t)(bj[e] - LS) * (D + 1);
                 for (int a = 0; a < D; ++a)
                     atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
                 atomicAdd(pp + D, 1ull);
@@ -1042,7 +1048,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
 #ifdef PCM_ABL_NOFLUSH
             const int nslots = 0;
 #else
-            const int nslots = h.mm < LSLOT ? h.mm : LSLOT;
+            const int nslots = h.mm < LS ? h.mm : LS;
 #endif
             const int npairs = nslots * (D + 1);
             // 16 threads per (slot, a) row, each summing AW/16 of its words
@@ -1067,11 +1073,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
                     atomicAdd(prep + (size_t)cid[par][slot] * (D + 1) + qq, (unsigned long long)sacc);
                 }
             }
-            if (kOvf && !h.full && h.mm > LSLOT)
-                for (int i = tid; i < (h.mm - LSLOT) * (D + 1); i += TPB) {
+            if (kOvf && !h.full && h.mm > LS)
+                for (int i = tid; i < (h.mm - LS) * (D + 1); i += TPB) {
                     const unsigned long long w = ovf[i];
                     if (w) {
-                        atomicAdd(prep + (size_t)cid[par][LSLOT + i / (D + 1)] * (D + 1) + i % (D + 1), w);
+                        atomicAdd(prep + (size_t)cid[par][LS + i / (D + 1)] * (D + 1) + i % (D + 1), w);
                         ovf[i] = 0ull;
                     }
                 }

@@ -286,3 +286,26 @@ def test_split_sequence_graph_replay(pcm, name):
     finally:
         dist.destroy_process_group()
     assert_same(res, ref, name + " graph")
+
+
+@pytest.mark.parametrize("slots", ["8", "16"])
+def test_lane_slot_variants(pcm, slots, monkeypatch):
+    """Both k_lloyd accumulation variants (8 lane slots + block-shared int64 LDS
+    words for list positions >= 8, or 16 lane slots + global atomics beyond)
+    on clouds whose lists are short (fine grid) and long (height-map cloud,
+    K=512 over few cells: positions well past 8 and 16)."""
+    monkeypatch.setenv("PCM_LSLOT_RT", slots)
+    X = R.splitmix_uniform(300_000, 3, 21)
+    C0 = X[R.init_indices(300_000, 24)]
+    ref = R.lloyd_fit(X, C0, max_iter=6, fast=True)
+    assert_same(gpu_fit(pcm, X, C0, 6), ref, f"short lists, {slots} slots")
+    rng = np.random.default_rng(22)
+    n = 120_000
+    y = rng.integers(0, 600, n).astype(np.float64)
+    x = rng.integers(0, 800, n).astype(np.float64)
+    z = 10 * np.sin(x / 90) + rng.normal(0, 0.5, n) + 30
+    X = np.stack([z, y, x], axis=1).astype(np.float32)
+    C0 = X[R.init_indices(n, 512)]
+    ref = R.lloyd_fit(X, C0, max_iter=6, fast=True)
+    res = gpu_fit(pcm, X, C0, 6)
+    assert_same(res, ref, f"long lists, {slots} slots")
