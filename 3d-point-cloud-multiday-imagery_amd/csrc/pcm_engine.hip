@@ -562,6 +562,17 @@ static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
     return (int)std::max(1LL, std::min<long long>(e->ntiles_cap, (long long)per_cu * e->num_cu));
 }
 
+// k_lloyd: one block per tile (the grid covers the layout's tile bound; blocks
+// past the device tile count exit at once).  Measured at config 3: 211 us per
+// launch vs 238 us for as many persistent blocks as are co-resident walking
+// tiles b, b + G, ... (the dispatcher keeps every CU's waves issuing point
+// loads; a persistent block waits on its own two-item prefetch); config-5
+// shape 485 vs 536 us; a 12.5M shard (2 tiles per resident block) unchanged.
+static int lloyd_grid(pcm_engine *e, const void *kern, size_t lds) {
+    if (std::getenv("PCM_ASSIGN_BLOCKS_PER_CU")) return assign_grid(e, kern, lds);   // tuning sweeps only
+    return (int)std::max(1LL, e->ntiles_cap);
+}
+
 static int lloyd_slots(const pcm_engine *e) {
     if (const char *ov = std::getenv("PCM_LSLOT_RT")) return std::atoi(ov) == 8 ? 8 : LSLOT;   // tuning sweeps only
     return (e->g.prune && e->g.ncells >= 8LL * e->k) ? 8 : LSLOT;
@@ -661,7 +672,7 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
             auto launch = [&](auto LSc) {
                 constexpr int LS = decltype(LSc)::value;
                 const size_t lds = (size_t)AccL<D, LS>::words * sizeof(uint32_t);
-                k_lloyd<TT, D, LS><<<assign_grid(e, (const void *)k_lloyd<TT, D, LS>, lds), TPB, lds, s>>>(
+                k_lloyd<TT, D, LS><<<lloyd_grid(e, (const void *)k_lloyd<TT, D, LS>, lds), TPB, lds, s>>>(
                     A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
             };
             if (D <= 3 && lloyd_slots(e) == 8) launch(std::integral_constant<int, 8>{});
@@ -705,7 +716,7 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
             double wmin = 0.0;
             for (int a = 0; a < D; ++a)
                 if (e->g.ext[a] > 0 && (wmin == 0.0 || e->g.w[a] < wmin)) wmin = e->g.w[a];
-            k_step<D><<<(int)(e->g.ncoarse * bpc + 1), CAND_TPB, lds, s>>>(
+            k_step<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, lds, s>>>(
                 e->g, from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->cref,
                 e->hist_changed, e->hist_shift, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab, bpc, e->drift_alpha,
                 e->drift_kappa * wmin);

@@ -64,6 +64,7 @@ struct Ctrl {
     double budget;                  // ... and the centre drift they tolerate (0: exact for the reference only)
     unsigned int rebuilds;          // candidate-list rebuilds of this fit (diagnostics)
     unsigned int pad1;
+    unsigned long long neq_acc;     // k_step: changed statistic words, summed over blocks (last arriver reads, resets)
 };
 
 // Fixed-point exponents q_a (identical on every rank).
@@ -335,6 +336,8 @@ template <int D> constexpr int cand_capc() { return D >= 4 ? 1024 : CAPC; }
 #endif
 constexpr int CAND_TPB = PCM_CAND_TPB;   // threads per candidate block (one child cell per wave at a time)
 constexpr int CAND_KBITS = 4096;         // bitmap capacity (larger K: direct ballot compaction)
+constexpr int CAND_CBW = 512;            // pair path: child bitmap words (4 KB)
+constexpr int CAND_MAXCH = 256;          // pair path: children per block
 constexpr int STEP_RB = 4;               // k_step: statistics rows per thread with loads in flight together
 
 #ifdef PCM_DBG_TIMING
@@ -372,6 +375,8 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     __shared__ unsigned long long kbits[CAND_KBITS / 64];
     __shared__ unsigned long long rkey;
     __shared__ uint32_t s_mp;
+    __shared__ unsigned long long cbits[CAND_CBW];   // pair path: per-child keep bitmaps over the coarse list
+    __shared__ uint32_t ckey[CAND_MAXCH];            // pair path: per-child reference key
     int ci[MAXD];
     decode(I, g.GC, D, ci);
     int nchild = 1;
@@ -391,6 +396,8 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         if (tid == 0) rkey = ~0ull;
         if (bitmap)
             for (int w = tid; w < CAND_KBITS / 64; w += CAND_TPB) kbits[w] = 0ull;
+        for (int w = tid; w < CAND_CBW; w += CAND_TPB) cbits[w] = 0ull;
+        for (int w = tid; w < CAND_MAXCH; w += CAND_TPB) ckey[w] = ~0u;
         __syncthreads();
         // reference key: fp32 bits of the max distance (any centre is a valid
         // reference; the key only ranks them) with the low 11 bits replaced by
@@ -461,10 +468,100 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     if (mp != 12345u) return;
 #endif
 
-    // ---- 2. one wave per child cell (F = 4 children per axis)
+    // ---- 2. children (F = 4 per axis) of this block: c0 .. c1-1
+    const int c0 = bsub * cpb, c1 = min(nchild, (bsub + 1) * cpb);
+    const int nwc = (int)((mp + 63u) / 64u);   // bitmap words per child
+    if (!pfull && c1 > c0 && (c1 - c0) <= CAND_MAXCH && (c1 - c0) * nwc <= CAND_CBW) {
+        // Pair path: one thread per (child, coarse-list position) in three
+        // block-wide passes -- (A) reference = a parent candidate nearest the
+        // child's centre (LDS atomic min of the key of the wave path below),
+        // (B) keep bits of the candidates that reference does not dominate,
+        // (C) ordered compaction (ascending centroid index) by popcounts.  The
+        // lists equal the wave path's; all pairs run in parallel instead of one
+        // child per wave after another (100M: 15 -> ~2 us per block).
+        const int nch = c1 - c0, npair = nch * (int)mp;
+        const int dch = CAND_TPB / (int)mp, dlp = CAND_TPB % (int)mp;
+        constexpr uint32_t LM = CAP > 256 ? 0x3FFu : 0xFFu;
+        auto child_cell = [&](int ch, int *f) -> bool {
+            bool inside = true;
+#pragma unroll
+            for (int a = D - 1, t = c0 + ch; a >= 0; --a, t >>= 2) {
+                f[a] = ci[a] * 4 + (t & 3);
+                inside &= f[a] < g.G[a];
+            }
+            return inside;
+        };
+        // (A)
+        for (int p = tid, ch = tid / (int)mp, l = tid % (int)mp; p < npair; p += CAND_TPB) {
+            int f[MAXD];
+            if (child_cell(ch, f)) {
+                double blo[MAXD], bhi[MAXD];
+                cell_box<D>(g, f, f, blo, bhi);
+                const float4 c = prec[l];
+                float dsum = 0.f;
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    const float dd = (float)(0.5 * (blo[a] + bhi[a])) - comp(c, a);
+                    dsum += dd * dd;
+                }
+                atomicMin(&ckey[ch], (__float_as_uint(dsum) & ~LM) | (uint32_t)l);
+            }
+            l += dlp;
+            ch += dch;
+            if (l >= (int)mp) { l -= (int)mp; ++ch; }
+        }
+        __syncthreads();
+        // (B)
+        for (int p = tid, ch = tid / (int)mp, l = tid % (int)mp; p < npair; p += CAND_TPB) {
+            int f[MAXD];
+            if (child_cell(ch, f)) {
+                double blo[MAXD], bhi[MAXD];
+                cell_box<D>(g, f, f, blo, bhi);
+                uint32_t bl = ckey[ch] & LM;
+                if (bl >= mp) bl = 0;
+                const float4 r = prec[bl];
+                const double mr = dl > 0.0 ? sqrt(maxdist<D>(blo, bhi, r)) : 0.0;
+                if (!prunable<D>(blo, bhi, prec[l], r, dl, mr))
+                    atomicOr(&cbits[ch * nwc + (l >> 6)], 1ull << (l & 63));
+            }
+            l += dlp;
+            ch += dch;
+            if (l >= (int)mp) { l -= (int)mp; ++ch; }
+        }
+        __syncthreads();
+        // (C)
+        for (int p = tid, ch = tid / (int)mp, l = tid % (int)mp; p < npair; p += CAND_TPB) {
+            int f[MAXD];
+            if (child_cell(ch, f)) {
+                const long long cell = encode(f, g.G, D);
+                const unsigned long long *wb = cbits + ch * nwc;
+                const unsigned long long word = wb[l >> 6];
+                uint32_t before = 0;
+                for (int w = 0; w < (l >> 6); ++w) before += __popcll(wb[w]);
+                if ((word >> (l & 63)) & 1ull) {
+                    const uint32_t pos = before + __popcll(word & ((1ull << (l & 63)) - 1ull));
+                    if (pos < (uint32_t)CAPF) {
+                        fc_rec[cell * CAPF + pos] = prec[l];
+                        fc_lab[cell * CAPF + pos] = pidx[l];
+                    }
+                }
+                if (l == 0) {
+                    uint32_t total = 0;
+                    for (int w = 0; w < nwc; ++w) total += __popcll(wb[w]);
+                    fc_cnt[cell] = total <= (uint32_t)CAPF ? total : FULL;
+                }
+            }
+            l += dlp;
+            ch += dch;
+            if (l >= (int)mp) { l -= (int)mp; ++ch; }
+        }
+        DBG_T(2);
+        return;
+    }
+    // wave path (FULL parent, or more pairs than the LDS bitmaps hold): one wave per child cell
     auto child = [&](auto PFc) {
         constexpr bool PF = decltype(PFc)::value;
-        for (int ch = bsub * cpb + wv; ch < min(nchild, (bsub + 1) * cpb); ch += CAND_TPB / 64) {
+        for (int ch = c0 + wv; ch < c1; ch += CAND_TPB / 64) {
             int f[MAXD];
             bool inside = true;
 #pragma unroll
@@ -1030,12 +1127,22 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
             for (int e = 0; e < 4; ++e) {
                 const bool v = whole || ((i0 + e >= h.start) && (i0 + e < h.end));
                 if (!(v && bj[e] >= LS)) continue;
-                // non-FULL: the block's LDS int64 words; FULL (all K): global int64
-                unsigned long long *pp = (h.full || !kOvf) ? prep + (size_t)(h.full ? bj[e] : cid[par][bj[e]]) * (D + 1)
-                                                           : ovf + (size_t)(bj[e] - LS) * (D + 1);
-                for (int a = 0; a < D; ++a)
-                    atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
-                atomicAdd(pp + D, 1ull);
+                // non-FULL: the block's LDS int64 words; FULL (all K): global int64.
+                // Two branches with one address space each: a pointer select
+                // would make these FLAT atomics, which count in vmcnt AND lgkmcnt
+                // and made the waitcnt pass drain every load (vmcnt(0)) before
+                // each work item's prefetch.
+                if (h.full || !kOvf) {
+                    unsigned long long *pp = prep + (size_t)(h.full ? bj[e] : cid[par][bj[e]]) * (D + 1);
+                    for (int a = 0; a < D; ++a)
+                        atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                    atomicAdd(pp + D, 1ull);
+                } else {
+                    const int o = (bj[e] - LS) * (D + 1);
+                    for (int a = 0; a < D; ++a)
+                        atomicAdd(&ovf[o + a], (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                    atomicAdd(&ovf[o + D], 1ull);
+                }
             }
         }
         if (!last_round) {
@@ -1082,7 +1189,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
                     }
                 }
         }
-        if (t + G >= nt) return false;
+        if (t + G >= nt) {
+            // The structurizer routes every step's exit through the loop latch, so
+            // the waitcnt pass merges this path's pending point loads into the
+            // loop header's state and would drain the whole pipeline (vmcnt(0))
+            // before each iteration's first prefetch.  Draining here (the block
+            // is done) keeps the header state that of the third step.
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+            return false;
+        }
         install(h1, par ^ 1);
         par ^= 1;
         h = h1;
@@ -1292,13 +1407,16 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
 //    alpha * (this iteration's largest centre shift), capped at kappa * the
 //    smallest cell width (above that: budget 0, exact lists).
 // The decision uses maxima over all K centres computed identically in every
-// block.  One extra block (the last) does the bookkeeping of k_global
-// (statistics-equality test, fixed-tree shift, history); the last block to
-// finish publishes C := new centres, the new reference/budget, the iteration
-// and the flags, and (stats_in) zeroes the all-reduce buffer for the next
-// accumulation.  An empty cluster halts (that block snapshots the statistics;
-// the host relocates, then k_global + k_cand resume).  stats_in: the
-// all-reduced statistics (multi-GPU) or nullptr = partials[parity] (single GPU).
+// block.  The bookkeeping of k_global is spread over the blocks: each block
+// owns a slice of the statistic words (statistics-equality test against the
+// previous iteration, relocation snapshot, zeroing the next parity half) and
+// every block keeps the per-lane shift sums of the fixed tree in registers.
+// The last block to finish reduces the tree, publishes C := new centres, the
+// new reference/budget, the history, the iteration and the flags, and
+// (stats_in) zeroes the all-reduce buffer for the next accumulation.  An
+// empty cluster halts (the host relocates, then k_global + k_cand resume).
+// stats_in: the all-reduced statistics (multi-GPU) or nullptr =
+// partials[parity] (single GPU).
 #ifndef PCM_STEP_WAVES
 #define PCM_STEP_WAVES 4   // >= 4 waves/SIMD (VGPR <= 128): 4 resident 256-thread blocks per CU
 #endif
@@ -1312,12 +1430,14 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
                                               double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl,
                                               uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
                                               int32_t *__restrict__ fc_lab, int bpc, double alpha, double dl_cap) {
+    static_assert(1024 % CAND_TPB == 0 && CAND_TPB >= 128, "shift tree: 1024 lanes over the block");
+    constexpr int NU = 1024 / CAND_TPB;   // shift-tree lanes L = tid + CAND_TPB * u per thread
     if (gated(ctrl)) return;
     DBG_T(0);
     extern __shared__ __attribute__((aligned(16))) float4 cn[];   // [K]
     __shared__ unsigned s_empty, s_last;
     __shared__ unsigned long long s_neq;
-    __shared__ double ssum[1024];
+    __shared__ double s_tree[CAND_TPB];
     __shared__ double s_dmax[CAND_TPB / 64], s_smax[CAND_TPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = K * (D + 1);
@@ -1326,16 +1446,22 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
     const double budget = ctrl->budget;
     const unsigned long long *src = stats_in ? stats_in : partials + (size_t)par * n;
     const float4 *ref = cref + (size_t)sel * K;
-    const bool b0 = blockIdx.x == gridDim.x - 1;   // the bookkeeping block (builds no candidate lists)
     if (tid == 0) { s_empty = 0; s_neq = 0ull; }
     __syncthreads();
     unsigned ne = 0;
-    unsigned long long neq = 0;
     double dmax = 0.0, smax = 0.0;   // squared drift from the reference / squared shift this iteration
+    // shift of centre j = tid + CAND_TPB * v added to tree lane L = j mod 1024,
+    // i.e. tacc[v % NU], in ascending j (the sequential per-lane sums of
+    // oracle/lloyd_ref.py shift_total); every block holds them, the last
+    // arriver reduces its own copy with the fixed tree.
+    double tacc[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) tacc[u] = 0.0;
     // rows j = tid + CAND_TPB * (j0 + u): STEP_RB rows' loads are all issued before any is used
     constexpr int RB = STEP_RB;
+    static_assert(RB % NU == 0, "row batches map onto tree lanes");
     for (int j0 = 0; j0 * CAND_TPB < K; j0 += RB) {
-        unsigned long long row[RB][D + 1], pv[RB][D + 1];
+        unsigned long long row[RB][D + 1];
         float4 rj[RB], oj[RB];
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
@@ -1345,9 +1471,6 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
             for (int a = 0; a <= D; ++a) row[u][a] = src[(size_t)jj * (D + 1) + a];
             rj[u] = ref[jj];
             oj[u] = C[jj];
-            if (b0)
-#pragma unroll
-                for (int a = 0; a <= D; ++a) pv[u][a] = prev[(size_t)jj * (D + 1) + a];
         }
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
@@ -1376,13 +1499,7 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
             }
             dmax = fmax(dmax, dr);
             smax = fmax(smax, ds);
-            if (b0) {   // convergence (sklearn: labels equal): raw statistics equal the previous ones
-#pragma unroll
-                for (int a = 0; a <= D; ++a) {
-                    neq += (row[u][a] != pv[u][a]) ? 1ull : 0ull;
-                    prev[(size_t)j * (D + 1) + a] = row[u][a];
-                }
-            }
+            tacc[u % NU] = tacc[u % NU] + ds;   // j0 is a multiple of RB, RB of NU
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -1391,27 +1508,30 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
     }
     if (lane == 0) { s_dmax[wv] = dmax; s_smax[wv] = smax; }
     if (ne) atomicAdd(&s_empty, ne);
-    if (neq) atomicAdd(&s_neq, neq);
     __syncthreads();
     DBG_T(6);
-    if (b0 && !stats_in)   // the next iteration accumulates into the other half
-        for (int i = tid; i < n; i += CAND_TPB) partials[(size_t)(par ^ 1u) * n + i] = 0ull;
-#if defined(PCM_ABL_NOHALT)
-    if (false) {   // ablation build: never halt (statistics are meaningless)
-#else
-    if (s_empty > 0) {
-#endif
-        if (b0) {
-            for (int i = tid; i < n; i += CAND_TPB) held[i] = src[i];
-            if (tid == 0) {
-                held[n] = 0ull;
-                ctrl->halt = 1u;
-                ctrl->n_empty = s_empty;
-                ctrl->neq_saved = s_neq;
-            }
+    // This block's slice of the statistic words: convergence (sklearn: labels
+    // equal) as raw statistics equal to the previous iteration's, the relocation
+    // snapshot, and (single GPU) zeroing the other parity half for the next
+    // accumulation.  The changed-word count reaches the last arriver through
+    // ctrl->neq_acc.
+    {
+        const bool halting = s_empty > 0;
+        unsigned long long *pnext = partials + (size_t)(par ^ 1u) * n;
+        for (int i = blockIdx.x * CAND_TPB + tid; i < n; i += gridDim.x * CAND_TPB) {
+            const unsigned long long v = src[i], pv = prev[i];
+            if (v != pv) atomicAdd(&s_neq, 1ull);
+            prev[i] = v;
+            if (!stats_in) pnext[i] = 0ull;
+            if (halting) held[i] = v;
         }
-        return;
+        if (halting && blockIdx.x == 0 && tid == 0) held[n] = 0ull;
     }
+#if defined(PCM_ABL_NOHALT)
+    const bool halt = false;   // ablation build: never halt (statistics are meaningless)
+#else
+    const bool halt = s_empty > 0;
+#endif
     dmax = s_dmax[0];
     smax = s_smax[0];
     for (int w = 1; w < CAND_TPB / 64; ++w) { dmax = fmax(dmax, s_dmax[w]); smax = fmax(smax, s_smax[w]); }
@@ -1419,87 +1539,85 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
     const bool rebuild = !(sqrt(dmax) * slack <= budget);
     double dl_new = alpha * sqrt(smax) * slack;
     if (!(dl_new <= dl_cap)) dl_new = 0.0;
-    if (b0) {
-        // shift with the fixed tree of k_global: lane L (0..1023) sums j = L + 1024 r
-        // sequentially; thread tid plays lanes tid + CAND_TPB u; then halving 512..1
-        for (int u = 0; u < 1024 / CAND_TPB; ++u) {
-            const int L = tid + CAND_TPB * u;
-            double acc = 0.0;
-            for (int j = L; j < K; j += 1024) {
-                const float4 a4 = cn[j], b4 = C[j];
-                double sh = 0.0;
-#pragma unroll
-                for (int a = 0; a < D; ++a) {
-                    const double dd = (double)comp(a4, a) - (double)comp(b4, a);
-                    const double sq = dd * dd;
-                    sh = (a == 0) ? sq : sh + sq;
-                }
-                acc = acc + sh;
-            }
-            ssum[L] = acc;
-        }
-        __syncthreads();
-        for (int st = 512; st >= 1; st >>= 1) {
-            for (int L = tid; L < st; L += CAND_TPB) ssum[L] = ssum[L] + ssum[L + st];
-            __syncthreads();
-        }
-        if (rebuild) {
-            float4 *nref = cref + (size_t)(sel ^ 1u) * K;
-            for (int j = tid; j < K; j += CAND_TPB) nref[j] = cn[j];
-        }
-        if (tid == 0) {
-            const uint32_t it = ctrl->iter;
-            if (it < ctrl->max_iter) {
-                hist_changed[it] = s_neq;
-                hist_shift[it] = ssum[0];
-            }
-            __hip_atomic_store(&ctrl->last_changed, s_neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctrl->last_shift, ssum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else if (rebuild) {
-        cand_body<D>(g, cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new);
-    } else {
-        refresh_body<D>(g, cn, fc_cnt, fc_rec, fc_lab, bpc);
+    if (!halt) {
+        if (rebuild) cand_body<D>(g, cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new);
+        else refresh_body<D>(g, cn, fc_cnt, fc_rec, fc_lab, bpc);
     }
     DBG_T(3);
-    // Every block has read ctrl (parity, reference, budget) and C before any
-    // block can observe the final count, so only the last block publishes.
-    // Nothing a block writes is read later in this launch except b0's
-    // last_changed / last_shift (sc1 stores, drained before b0's arrival, read
-    // with sc1 loads by the last arriver: MI355X_MICROARCH.md hand-off row 1),
-    // so the arrival needs no L2 write-back fence.
+    // Arrival.  Every block has read ctrl (parity, reference, budget) and C
+    // before any block can observe the final count, so only the last block
+    // publishes.  The only value written in this launch and read later in it
+    // is neq_acc (an L2 atomic drained by s_waitcnt before the arrival, read
+    // with an agent-scope load by the last arriver), so the arrival needs no
+    // L2 write-back fence (MI355X_MICROARCH.md hand-off row 1).
     __syncthreads();
     if (tid == 0) {
+        if (s_neq) __hip_atomic_fetch_add(&ctrl->neq_acc, s_neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prior = __hip_atomic_fetch_add(&ctrl->step_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (prior == gridDim.x - 1) ? 1u : 0u;
     }
     __syncthreads();
     if (!s_last) return;
+    const unsigned long long changed = __hip_atomic_load(&ctrl->neq_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (halt) {   // empty cluster: the host relocates, then k_global + k_cand resume
+        if (tid == 0) {
+            ctrl->step_done = 0u;
+            ctrl->neq_acc = 0ull;
+            ctrl->n_empty = s_empty;
+            ctrl->neq_saved = changed;
+            ctrl->halt = 1u;
+        }
+        return;
+    }
+    // total shift: the fixed tree of k_global / oracle shift_total over 1024 lanes
+#pragma unroll
+    for (int st = 512, h = NU / 2; st >= CAND_TPB; st >>= 1, h >>= 1)
+#pragma unroll
+        for (int u = 0; u < h; ++u) tacc[u] = tacc[u] + tacc[u + h];
+    s_tree[tid] = tacc[0];
     for (int j = tid; j < K; j += CAND_TPB) C[j] = cn[j];
+    if (rebuild) {
+        float4 *nref = cref + (size_t)(sel ^ 1u) * K;
+        for (int j = tid; j < K; j += CAND_TPB) nref[j] = cn[j];
+    }
     if (stats_in)   // every block has read the all-reduced statistics: zero them for the next accumulation
         for (int i = tid; i < n + 1; i += CAND_TPB) stats_in[i] = 0ull;
-    if (tid == 0) {
-        const unsigned long long changed =
-            __hip_atomic_load(&ctrl->last_changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double shift = __hip_atomic_load(&ctrl->last_shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t it = ctrl->iter;
-        ctrl->step_done = 0u;
-        ctrl->resume = 0u;
-        if (rebuild) {
-            ctrl->ref_sel = sel ^ 1u;
-            ctrl->budget = dl_new;
-            ctrl->rebuilds += 1u;
-        }
-        uint32_t done = 0;
-        if (changed == 0ull) done = 1u;
-        else if (shift <= ctrl->tol) done = 2u;
+    __syncthreads();
+    for (int st = CAND_TPB / 2; st >= 64; st >>= 1) {
+        if (tid < st) s_tree[tid] = s_tree[tid] + s_tree[tid + st];
+        __syncthreads();
+    }
+    if (wv == 0) {
+        double v = s_tree[lane];
+        for (int st = 32; st > 0; st >>= 1) v = v + __shfl_down(v, st);   // lane t: v_t + v_{t+st}
+        if (lane == 0) {
+            const double shift = v;
+            const uint32_t it = ctrl->iter;
+            if (it < ctrl->max_iter) {
+                hist_changed[it] = changed;
+                hist_shift[it] = shift;
+            }
+            ctrl->last_changed = changed;
+            ctrl->last_shift = shift;
+            ctrl->step_done = 0u;
+            ctrl->neq_acc = 0ull;
+            ctrl->resume = 0u;
+            if (rebuild) {
+                ctrl->ref_sel = sel ^ 1u;
+                ctrl->budget = dl_new;
+                ctrl->rebuilds += 1u;
+            }
+            uint32_t done = 0;
+            if (changed == 0ull) done = 1u;
+            else if (shift <= ctrl->tol) done = 2u;
 #if defined(PCM_ABL_NOHALT)
-        done = 0u;
+            done = 0u;
 #endif
-        if (!done && it + 1 >= ctrl->max_iter) done = 3u;
-        ctrl->done = done;
-        ctrl->iter = it + 1;
+            if (!done && it + 1 >= ctrl->max_iter) done = 3u;
+            ctrl->done = done;
+            ctrl->iter = it + 1;
+        }
     }
     DBG_T(7);
 }

@@ -29,12 +29,10 @@ t0 = t[:, 0].min()
 us = lambda v: v / 100.0   # s_memrealtime: 100 MHz
 print(f"iters {st['iter']} rebuilds {st['list_rebuilds']} blocks {nbk}")
 print("block start spread us: p50 %.1f p90 %.1f max %.1f" % tuple(us(np.percentile(t[:, 0] - t0, q)) for q in (50, 90, 100)))
-w = t[:-1]
+w = t
 print("centres+drift us (start->6): p50 %.1f max %.1f" % (us(np.median(w[:, 6] - w[:, 0])), us((w[:, 6] - w[:, 0]).max())))
 print("body us (6->3): p50 %.1f max %.1f" % (us(np.median(w[:, 3] - w[:, 6])), us((w[:, 3] - w[:, 6]).max())))
-b = t[-1]
-print("b0: centres %.1f, bookkeeping %.1f us" % (us(b[6] - b[0]), us(b[3] - b[6])))
-c = t[:-1]
+c = t
 for k0, k1, name in ((6, 4, "coarse reference"), (4, 5, "coarse prune"), (5, 1, "coarse compact"), (1, 2, "children")):
     ok = (c[:, k0] > 0) & (c[:, k1] > 0)
     if ok.any():

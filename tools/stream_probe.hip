@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void k_chunk(const float *xs, unsigned short *
 }
 
 // persistent: G blocks stride over chunks, two chunks in flight (ping-pong)
-template <int WRITE>
+template <int WRITE, int LAB = 1>
 __global__ __launch_bounds__(256) void k_persist(const float *xs, unsigned short *lab, unsigned n, unsigned nchunk,
                                                  unsigned *sink) {
     const rsrc_t rx = mk(xs, n * 12u), rl = mk(lab, n * 2u);
@@ -44,7 +44,8 @@ __global__ __launch_bounds__(256) void k_persist(const float *xs, unsigned short
         a[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u, 0, 0);
         b[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u + 16u, 0, 0);
         c[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, p * 12u + 32u, 0, 0);
-        l[s] = __builtin_amdgcn_raw_buffer_load_b64(rl, p * 2u, 0, 0);
+        if (LAB) l[s] = __builtin_amdgcn_raw_buffer_load_b64(rl, p * 2u, 0, 0);
+        else l[s] = u32x2{0u, 0u};
     };
     auto use = [&](int s, unsigned chunk) {
         const unsigned p = chunk * 1024u + 4u * threadIdx.x;
@@ -103,6 +104,8 @@ int main(int argc, char **argv) {
         run(nm, rw, [&] { k_persist<1><<<256 * bpc, 256>>>(xs, lab, n, nchunk, sink); });
         snprintf(nm, sizeof nm, "persist read %d/CU", bpc);
         run(nm, ro, [&] { k_persist<0><<<256 * bpc, 256>>>(xs, lab, n, nchunk, sink); });
+        snprintf(nm, sizeof nm, "persist read12 %d/CU", bpc);
+        run(nm, (double)n * 12, [&] { k_persist<0, 0><<<256 * bpc, 256>>>(xs, lab, n, nchunk, sink); });
     }
     return 0;
 }
