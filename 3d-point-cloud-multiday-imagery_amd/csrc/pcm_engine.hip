@@ -562,16 +562,13 @@ static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
     return (int)std::max(1LL, std::min<long long>(e->ntiles_cap, (long long)per_cu * e->num_cu));
 }
 
-// k_lloyd: one block per tile (the grid covers the layout's tile bound; blocks
+// k_lloyd1: one block per tile (the grid covers the layout's tile bound; blocks
 // past the device tile count exit at once).  Measured at config 3: 211 us per
-// launch vs 238 us for as many persistent blocks as are co-resident walking
-// tiles b, b + G, ... (the dispatcher keeps every CU's waves issuing point
-// loads; a persistent block waits on its own two-item prefetch); config-5
-// shape 485 vs 536 us; a 12.5M shard (2 tiles per resident block) unchanged.
-static int lloyd_grid(pcm_engine *e, const void *kern, size_t lds) {
-    if (std::getenv("PCM_ASSIGN_BLOCKS_PER_CU")) return assign_grid(e, kern, lds);   // tuning sweeps only
-    return (int)std::max(1LL, e->ntiles_cap);
-}
+// launch for k_lloyd with one tile per block vs 238 us for as many persistent
+// blocks as are co-resident walking tiles b, b + G, ... (each tile's list
+// install stalled its block; with one tile per block the other resident blocks
+// keep streaming); config-5 shape 485 vs 536 us.
+static int lloyd_grid(const pcm_engine *e) { return (int)std::max(1LL, e->ntiles_cap); }
 
 static int lloyd_slots(const pcm_engine *e) {
     if (const char *ov = std::getenv("PCM_LSLOT_RT")) return std::atoi(ov) == 8 ? 8 : LSLOT;   // tuning sweeps only
@@ -672,8 +669,12 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
             auto launch = [&](auto LSc) {
                 constexpr int LS = decltype(LSc)::value;
                 const size_t lds = (size_t)AccL<D, LS>::words * sizeof(uint32_t);
-                k_lloyd<TT, D, LS><<<lloyd_grid(e, (const void *)k_lloyd<TT, D, LS>, lds), TPB, lds, s>>>(
-                    A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
+                if (std::getenv("PCM_ASSIGN_BLOCKS_PER_CU"))   // persistent tile walk (tuning sweeps only)
+                    k_lloyd<TT, D, LS><<<assign_grid(e, (const void *)k_lloyd<TT, D, LS>, lds), TPB, lds, s>>>(
+                        A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
+                else
+                    k_lloyd1<TT, D, LS><<<lloyd_grid(e), TPB, lds, s>>>(A, e->tiles, e->fc_rec, e->fc_lab, e->C,
+                                                                          e->fc_cnt);
             };
             if (D <= 3 && lloyd_slots(e) == 8) launch(std::integral_constant<int, 8>{});
             else launch(std::integral_constant<int, LSLOT>{});
@@ -1148,6 +1149,10 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
 #ifdef PCM_DBG_TIMING
 int pcm_debug_timing(unsigned long long *out, int nblocks) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_t), (size_t)nblocks * 8 * sizeof(unsigned long long)));
+    return 0;
+}
+int pcm_debug_timing_lloyd(unsigned long long *out, int nblocks) {
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_l), (size_t)nblocks * 4 * sizeof(unsigned long long)));
     return 0;
 }
 #endif

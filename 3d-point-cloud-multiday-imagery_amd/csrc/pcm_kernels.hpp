@@ -343,8 +343,11 @@ constexpr int STEP_RB = 4;               // k_step: statistics rows per thread w
 #ifdef PCM_DBG_TIMING
 __device__ unsigned long long g_dbg_t[8192][8];
 #define DBG_T(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ unsigned long long g_dbg_l[65536][4];
+#define DBG_L(k) do { if (threadIdx.x == 0 && blockIdx.x < 65536) g_dbg_l[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define DBG_T(k) do { } while (0)
+#define DBG_L(k) do { } while (0)
 #endif
 
 // Wave-wide minimum through DPP (row_shr 1/2/4/8 scan, then row_bcast 15/31;
@@ -420,19 +423,30 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                 if (!prunable<D>(blo, bhi, C[j], r, dl, mr)) atomicOr(&kbits[j >> 6], 1ull << (j & 63));
             __syncthreads();
             DBG_T(5);
+            // ordered compaction: word prefix counts by one wave-wide scan, then
+            // every wave compacts the words w = wv (mod waves) in parallel
+            __shared__ uint32_t wpre[CAND_KBITS / 64];
+            const int nwk = (K + 63) / 64;   // <= 64
             if (wv == 0) {
-                uint32_t total = 0;
-                for (int w = 0; w < (K + 63) / 64; ++w) {
-                    const unsigned long long word = kbits[w];
-                    const uint32_t pos = total + __popcll(word & ((1ull << lane) - 1ull));
-                    const int j = w * 64 + lane;
-                    if (((word >> lane) & 1ull) && pos < (uint32_t)CAP) {
-                        prec[pos] = C[j];
-                        pidx[pos] = j;
-                    }
-                    total += __popcll(word);
+                const uint32_t c = lane < nwk ? (uint32_t)__popcll(kbits[lane]) : 0u;
+                uint32_t x = c;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(x, o);
+                    if (lane >= o) x += y;
                 }
-                if (lane == 0) s_mp = total <= (uint32_t)CAP ? total : FULL;
+                wpre[lane] = x - c;
+                if (lane == 63) s_mp = x <= (uint32_t)CAP ? x : FULL;
+            }
+            __syncthreads();
+            for (int w = wv; w < nwk; w += CAND_TPB / 64) {
+                const unsigned long long word = kbits[w];
+                const uint32_t pos = wpre[w] + __popcll(word & ((1ull << lane) - 1ull));
+                const int j = w * 64 + lane;
+                if (((word >> lane) & 1ull) && pos < (uint32_t)CAP) {
+                    prec[pos] = C[j];
+                    pidx[pos] = j;
+                }
             }
         } else {
             // large K: ordered compaction by ballots (one barrier pair per CAND_TPB centres)
@@ -471,7 +485,10 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     // ---- 2. children (F = 4 per axis) of this block: c0 .. c1-1
     const int c0 = bsub * cpb, c1 = min(nchild, (bsub + 1) * cpb);
     const int nwc = (int)((mp + 63u) / 64u);   // bitmap words per child
-    if (!pfull && c1 > c0 && (c1 - c0) <= CAND_MAXCH && (c1 - c0) * nwc <= CAND_CBW) {
+    // pair path when each wave would otherwise walk >= 8 children one after the
+    // other (100M: 64 children per block, 15 -> 9.6 us); with few children per
+    // block (12.5M shard: 8) the wave path's two chains per wave are shorter
+    if (!pfull && (c1 - c0) >= 2 * CAND_TPB / 16 && (c1 - c0) <= CAND_MAXCH && (c1 - c0) * nwc <= CAND_CBW) {
         // Pair path: one thread per (child, coarse-list position) in three
         // block-wide passes -- (A) reference = a parent candidate nearest the
         // child's centre (LDS atomic min of the key of the wave path below),
@@ -1011,6 +1028,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     const unsigned nt = *A.ntiles;
     unsigned t = blockIdx.x;
     if (t >= nt) return;
+    DBG_L(0);
     const float4 *lrec = fc_rec;
     const int32_t *llab = fc_lab;
     // tile record with .w := the cell's candidate count (dependent scalar load)
@@ -1080,6 +1098,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     LOAD_X(xa, item_off(0));
     LOAD_X(xb, item_off(1));
     __syncthreads();
+    DBG_L(1);
 
     unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.pstride;
     int par = 0;
@@ -1150,6 +1169,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
             return true;
         }
         // ---- tile boundary: fold the slot sums of h, install h1's candidates
+        DBG_L(2);
         __syncthreads();
         {
 #ifdef PCM_ABL_NOFLUSH
@@ -1190,6 +1210,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
                 }
         }
         if (t + G >= nt) {
+            DBG_L(3);
             // The structurizer routes every step's exit through the loop latch, so
             // the waitcnt pass merges this path's pending point loads into the
             // loop header's state and would drain the whole pipeline (vmcnt(0))
@@ -1214,6 +1235,187 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         if (!step(xb, xa)) break;
         if (!step(xc, xb)) break;
     }
+}
+
+// One Lloyd iteration's E-step + accumulation, ONE TILE PER BLOCK (the
+// default launch).  Same arithmetic, slots and fold as k_lloyd; what differs
+// is the block's start-up: the tile record, the candidate count and the first
+// LSPEC list records (vector loads, speculative: the count is not known yet)
+// and the first two work items' point loads are all issued before anything
+// is waited for, so a block starts scanning one point-load latency after it
+// starts (the tile record -> count -> records chain cost ~3.8 us per block,
+// a quarter of its lifetime at config 3).  The list loads precede the point
+// loads, so the in-order vmcnt wait for the first work item covers them.
+constexpr int LSPEC = 16;   // list records loaded before the count is known
+template <typename T, int D, int LS>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8))) void k_lloyd1(
+    LloydArgs A, const uint4 *__restrict__ tiles, const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
+    const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt) {
+    if (gated(A.ctrl)) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LS+1)*(D+1)][AW]
+    __shared__ float4 crec[CAPF];
+    __shared__ int32_t cid[CAPF];
+#ifdef PCM_OVF_ALL
+    constexpr bool kOvf = true;
+#else
+    constexpr bool kOvf = D >= 4 || LS < LSLOT;
+#endif
+    __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
+    const int tid = threadIdx.x;
+    const unsigned t = blockIdx.x;
+    // the tiles buffer holds ntiles_cap >= gridDim.x records: the load is in
+    // bounds before the device tile count says whether this block has work
+    const uint4 tr = tiles[t];
+    const unsigned nt = *A.ntiles;
+    if (t >= nt) return;
+    DBG_L(0);
+    const unsigned cell = tr.x, start = tr.y, end = tr.z;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f);
+    int l0 = 0;
+    if (tid < LSPEC) {
+        r0 = fc_rec[(size_t)cell * CAPF + tid];
+        l0 = fc_lab[(size_t)cell * CAPF + tid];
+    }
+    const uint32_t cnt = fc_cnt[cell];
+    const unsigned base0 = start & ~3u;
+    const int nr = (int)((end - base0 + 4 * TPB - 1) / (4 * TPB));
+    const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
+    // lanes past the tile's end get the out-of-range offset: zeros, no memory traffic
+    auto item_off = [&](int rr) -> unsigned {
+        const unsigned o = base0 + (unsigned)rr * 4u * TPB + 4u * tid;
+        return (rr < nr && o < end) ? o : 0x0ffffff0u;
+    };
+    Raw<T, D> xa, xb, xc;
+    LOAD_X(xa, item_off(0));
+    LOAD_X(xb, item_off(1));
+    for (int e = tid; e < AccL<D, LS>::words; e += TPB) acc[e] = 0u;
+    if (kOvf)
+        for (int e = tid; e < (CAPF - LS) * (D + 1); e += TPB) ovf[e] = 0ull;
+    const bool full = (cnt == FULL);
+    const int mm = full ? A.K : (int)cnt;
+    if (full) {
+        if (tid < LS) cid[tid] = tid;
+    } else {
+        if (tid < LSPEC && tid < mm) {
+            crec[tid] = r0;
+            cid[tid] = l0;
+        }
+        for (int j = LSPEC + tid; j < mm; j += TPB) {   // long lists (rare at D <= 3)
+            crec[j] = fc_rec[(size_t)cell * CAPF + j];
+            cid[j] = fc_lab[(size_t)cell * CAPF + j];
+        }
+    }
+    uint32_t *const myacc = acc + (tid & (AW - 1));
+    unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.pstride;
+    __syncthreads();
+    DBG_L(1);
+
+    // loads per work item; after item r+2's are issued, items r+1 and r+2 may
+    // stay outstanding while r is computed
+    constexpr int NL = Raw<T, D>::NW / 4 + (Raw<T, D>::NW % 4 ? 1 : 0);
+    constexpr int VM = 2 * NL;
+    constexpr int WAIT_PREV = 0x0F70 | (VM & 0xF) | ((VM >> 4) << 14);   // vmcnt(VM) expcnt(7) lgkmcnt(15)
+    auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx, int r) {
+        LOAD_X(nx, item_off(r + 2));
+        if (r >= nr) {
+            // padding step (nr not a multiple of 3): no compute, but the same
+            // wait as a computing step, so that every path reaches the loop
+            // latch with the same outstanding loads (a skipped step left the
+            // waitcnt pass a pessimistic merge: vmcnt(0) before each prefetch)
+            __builtin_amdgcn_s_waitcnt(WAIT_PREV);
+            return;
+        }
+        const unsigned rbase = base0 + (unsigned)r * 4u * TPB;
+        const unsigned i0 = rbase + 4u * tid;
+        float x[4][D];
+        unpack_x<D>(cx, x);
+        int bj[4];
+#ifdef PCM_ABL_NOSCAN
+        if (true) {
+#else
+        if (mm == 1) {
+#endif
+            for (int e = 0; e < 4; ++e) bj[e] = 0;
+        } else {
+            float bd[4];
+            if (full) scan4_s<D>(Call, mm, x, bd, bj);
+            else scan4<D>(crec, mm, x, bd, bj);
+        }
+        // block-uniform: every point of the round lies inside the tile
+        const bool whole = (rbase >= start) && (rbase + 4u * TPB <= end);
+        int sl[4];
+        bool over = false;
+        for (int e = 0; e < 4; ++e) {
+            const bool v = whole || ((i0 + e >= start) && (i0 + e < end));
+            const bool hi = bj[e] >= LS;
+            over |= v && hi;
+            sl[e] = (v && !hi) ? bj[e] : LS;
+        }
+        for (int e = 0; e < 4; ++e) {
+            uint32_t *ap = myacc + sl[e] * ((D + 1) * AW);
+            for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
+            atomicAdd(ap + D * AW, 1u);
+        }
+        if (over) {   // list positions >= LS (long lists only)
+            for (int e = 0; e < 4; ++e) {
+                const bool v = whole || ((i0 + e >= start) && (i0 + e < end));
+                if (!(v && bj[e] >= LS)) continue;
+                // one address space per branch (a pointer select would make FLAT
+                // atomics, which count in vmcnt and lgkmcnt and drain the prefetch)
+                if (full || !kOvf) {
+                    unsigned long long *pp = prep + (size_t)(full ? bj[e] : cid[bj[e]]) * (D + 1);
+                    for (int a = 0; a < D; ++a)
+                        atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                    atomicAdd(pp + D, 1ull);
+                } else {
+                    const int o = (bj[e] - LS) * (D + 1);
+                    for (int a = 0; a < D; ++a)
+                        atomicAdd(&ovf[o + a], (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                    atomicAdd(&ovf[o + D], 1ull);
+                }
+            }
+        }
+    };
+    // three rotating register sets: work items r+1 and r+2 in flight while r is
+    // computed; a tile holds at most TILE / (4 TPB) = 8 rounds
+    for (int r = 0; r < nr; r += 3) {
+        step(xa, xc, r);
+        step(xb, xa, r + 1);
+        step(xc, xb, r + 2);
+    }
+    DBG_L(2);
+    // fold the slot words into the int64 statistics: 16 threads per (slot, a) row
+    __syncthreads();
+    {
+        const int nslots = mm < LS ? mm : LS;
+        const int npairs = nslots * (D + 1);
+        for (int p0 = 0; p0 < npairs; p0 += TPB / 16) {
+            const int pi = p0 + tid / 16, sub = tid & 15;
+            long long sacc = 0;
+            if (pi < npairs) {
+                const bool isc = (pi % (D + 1) == D);
+                const uint32_t *row = acc + pi * AW;
+                for (int k = 0; k < AW / 16; ++k) {
+                    const uint32_t w = row[sub + 16 * k];
+                    sacc += isc ? (long long)w : (long long)(int32_t)w;
+                }
+            }
+            sacc += __shfl_down(sacc, 8, 16);
+            sacc += __shfl_down(sacc, 4, 16);
+            sacc += __shfl_down(sacc, 2, 16);
+            sacc += __shfl_down(sacc, 1, 16);
+            if (pi < npairs && sub == 0 && sacc) {
+                const int slot = pi / (D + 1), qq = pi % (D + 1);
+                atomicAdd(prep + (size_t)cid[slot] * (D + 1) + qq, (unsigned long long)sacc);
+            }
+        }
+        if (kOvf && !full && mm > LS)
+            for (int i = tid; i < (mm - LS) * (D + 1); i += TPB) {
+                const unsigned long long w = ovf[i];
+                if (w) atomicAdd(prep + (size_t)cid[LS + i / (D + 1)] * (D + 1) + i % (D + 1), w);
+            }
+    }
+    DBG_L(3);
 }
 
 // Single block of 1024 threads.  Optionally first folds partials[parity] into
