@@ -1148,7 +1148,7 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
 
 #ifdef PCM_DBG_TIMING
 int pcm_debug_timing(unsigned long long *out, int nblocks) {
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_t), (size_t)nblocks * 8 * sizeof(unsigned long long)));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_t), (size_t)nblocks * 16 * sizeof(unsigned long long)));
     return 0;
 }
 int pcm_debug_timing_lloyd(unsigned long long *out, int nblocks) {

@@ -21,7 +21,7 @@
 namespace pcm {
 
 constexpr int MAXD = 4;
-constexpr int CAPC = 256;          // coarse candidate capacity
+constexpr int CAPC = 512;          // coarse candidate capacity (12.5M shard: coarse lists p90 243, max > 256)
 constexpr int CAPF = 64;           // fine candidate capacity
 constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-centre ranks)
 #ifndef PCM_TPB
@@ -332,21 +332,23 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
 // D = 4: a coarse cell has 4^4 = 256 fine cells and a longer coarse list
 template <int D> constexpr int cand_capc() { return D >= 4 ? 1024 : CAPC; }
 #ifndef PCM_CAND_TPB
-#define PCM_CAND_TPB 256
+#define PCM_CAND_TPB 512   // k_step at config 3: 25.7 vs 28.7 us (the pair passes are latency-bound)
 #endif
 constexpr int CAND_TPB = PCM_CAND_TPB;   // threads per candidate block (one child cell per wave at a time)
 constexpr int CAND_KBITS = 4096;         // bitmap capacity (larger K: direct ballot compaction)
 constexpr int CAND_CBW = 512;            // pair path: child bitmap words (4 KB)
-constexpr int CAND_MAXCH = 256;          // pair path: children per block
+constexpr int CAND_MAXCH = 64;           // pair path: children per block
 constexpr int STEP_RB = 4;               // k_step: statistics rows per thread with loads in flight together
 
 #ifdef PCM_DBG_TIMING
-__device__ unsigned long long g_dbg_t[8192][8];
+__device__ unsigned long long g_dbg_t[8192][16];
 #define DBG_T(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define DBG_V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = (unsigned long long)(v); } while (0)
 __device__ unsigned long long g_dbg_l[65536][4];
 #define DBG_L(k) do { if (threadIdx.x == 0 && blockIdx.x < 65536) g_dbg_l[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define DBG_T(k) do { } while (0)
+#define DBG_V(k, v) do { } while (0)
 #define DBG_L(k) do { } while (0)
 #endif
 
@@ -379,7 +381,6 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     __shared__ unsigned long long rkey;
     __shared__ uint32_t s_mp;
     __shared__ unsigned long long cbits[CAND_CBW];   // pair path: per-child keep bitmaps over the coarse list
-    __shared__ uint32_t ckey[CAND_MAXCH];            // pair path: per-child reference key
     int ci[MAXD];
     decode(I, g.GC, D, ci);
     int nchild = 1;
@@ -400,7 +401,6 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         if (bitmap)
             for (int w = tid; w < CAND_KBITS / 64; w += CAND_TPB) kbits[w] = 0ull;
         for (int w = tid; w < CAND_CBW; w += CAND_TPB) cbits[w] = 0ull;
-        for (int w = tid; w < CAND_MAXCH; w += CAND_TPB) ckey[w] = ~0u;
         __syncthreads();
         // reference key: fp32 bits of the max distance (any centre is a valid
         // reference; the key only ranks them) with the low 11 bits replaced by
@@ -478,6 +478,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     const bool pfull = (mp == FULL);
     if (pfull) mp = (uint32_t)K;
     DBG_T(1);
+    DBG_V(8, mp);
 #ifdef PCM_ABL_COARSEONLY
     if (mp != 12345u) return;
 #endif
@@ -499,58 +500,105 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         const int nch = c1 - c0, npair = nch * (int)mp;
         const int dch = CAND_TPB / (int)mp, dlp = CAND_TPB % (int)mp;
         constexpr uint32_t LM = CAP > 256 ? 0x3FFu : 0xFFu;
-        auto child_cell = [&](int ch, int *f) -> bool {
+        // (0) per-child cell id, fp64 box and centre, once per child
+        __shared__ double s_blo[CAND_MAXCH][D], s_bhi[CAND_MAXCH][D];
+        __shared__ float s_ctr[CAND_MAXCH][D];
+        __shared__ long long s_cell[CAND_MAXCH];
+        __shared__ float4 s_ref[CAND_MAXCH];   // the child's reference centre (pass A)
+        __shared__ double s_mr[CAND_MAXCH];    // max distance from the child's box to it (drift budget > 0)
+        for (int ch = tid; ch < nch; ch += CAND_TPB) {
+            int f[MAXD];
             bool inside = true;
 #pragma unroll
             for (int a = D - 1, t = c0 + ch; a >= 0; --a, t >>= 2) {
                 f[a] = ci[a] * 4 + (t & 3);
                 inside &= f[a] < g.G[a];
             }
-            return inside;
-        };
-        // (A)
-        for (int p = tid, ch = tid / (int)mp, l = tid % (int)mp; p < npair; p += CAND_TPB) {
-            int f[MAXD];
-            if (child_cell(ch, f)) {
-                double blo[MAXD], bhi[MAXD];
-                cell_box<D>(g, f, f, blo, bhi);
-                const float4 c = prec[l];
-                float dsum = 0.f;
+            double blo[MAXD], bhi[MAXD];
+            cell_box<D>(g, f, f, blo, bhi);
 #pragma unroll
-                for (int a = 0; a < D; ++a) {
-                    const float dd = (float)(0.5 * (blo[a] + bhi[a])) - comp(c, a);
-                    dsum += dd * dd;
-                }
-                atomicMin(&ckey[ch], (__float_as_uint(dsum) & ~LM) | (uint32_t)l);
+            for (int a = 0; a < D; ++a) {
+                s_blo[ch][a] = blo[a];
+                s_bhi[ch][a] = bhi[a];
+                s_ctr[ch][a] = (float)(0.5 * (blo[a] + bhi[a]));
             }
-            l += dlp;
-            ch += dch;
-            if (l >= (int)mp) { l -= (int)mp; ++ch; }
+            s_cell[ch] = inside ? encode(f, g.G, D) : -1ll;
         }
         __syncthreads();
-        // (B)
-        for (int p = tid, ch = tid / (int)mp, l = tid % (int)mp; p < npair; p += CAND_TPB) {
-            int f[MAXD];
-            if (child_cell(ch, f)) {
-                double blo[MAXD], bhi[MAXD];
-                cell_box<D>(g, f, f, blo, bhi);
-                uint32_t bl = ckey[ch] & LM;
+        DBG_T(10);
+        // (A) reference per child: TPC threads per child scan its share of
+        // the coarse list, then a min over the TPC lanes (shuffles, no atomics:
+        // an LDS atomic per pair serialised ~25-way on the child's word)
+        {
+            int tpc = 64;
+            while (tpc > 1 && tpc * nch > CAND_TPB) tpc >>= 1;
+            const int ch = tid / tpc, sub = tid % tpc;
+            uint32_t best = ~0u;
+            if (ch < nch && s_cell[ch] >= 0)
+                for (int l = sub; l < (int)mp; l += tpc) {
+                    const float4 c = prec[l];
+                    float dsum = 0.f;
+#pragma unroll
+                    for (int a = 0; a < D; ++a) {
+                        const float dd = s_ctr[ch][a] - comp(c, a);
+                        dsum += dd * dd;
+                    }
+                    const uint32_t key = (__float_as_uint(dsum) & ~LM) | (uint32_t)l;
+                    best = key < best ? key : best;
+                }
+            for (int o = 1; o < tpc; o <<= 1) {
+                const uint32_t ob = (uint32_t)__shfl_xor((int)best, o);
+                best = ob < best ? ob : best;
+            }
+            if (ch < nch && sub == 0 && s_cell[ch] >= 0) {
+                uint32_t bl = best & LM;
                 if (bl >= mp) bl = 0;
                 const float4 r = prec[bl];
-                const double mr = dl > 0.0 ? sqrt(maxdist<D>(blo, bhi, r)) : 0.0;
-                if (!prunable<D>(blo, bhi, prec[l], r, dl, mr))
-                    atomicOr(&cbits[ch * nwc + (l >> 6)], 1ull << (l & 63));
+                s_ref[ch] = r;
+                if (dl > 0.0) {
+                    double blo[MAXD], bhi[MAXD];
+#pragma unroll
+                    for (int a = 0; a < D; ++a) { blo[a] = s_blo[ch][a]; bhi[a] = s_bhi[ch][a]; }
+                    s_mr[ch] = sqrt(maxdist<D>(blo, bhi, r));
+                } else {
+                    s_mr[ch] = 0.0;
+                }
             }
-            l += dlp;
-            ch += dch;
-            if (l >= (int)mp) { l -= (int)mp; ++ch; }
         }
         __syncthreads();
+        DBG_T(11);
+        // (B) keep bits; the lanes of one (child, bitmap word) are contiguous in a
+        // wave, so one ballot and one LDS atomic per segment
+        {
+            const int iters = (npair + CAND_TPB - 1) / CAND_TPB;
+            int ch = tid / (int)mp, l = tid % (int)mp;
+            for (int it = 0, p = tid; it < iters; ++it, p += CAND_TPB) {
+                bool keep = false;
+                const bool valid = p < npair && s_cell[ch < nch ? ch : 0] >= 0 && ch < nch;
+                if (valid) {
+                    double blo[MAXD], bhi[MAXD];
+#pragma unroll
+                    for (int a = 0; a < D; ++a) { blo[a] = s_blo[ch][a]; bhi[a] = s_bhi[ch][a]; }
+                    keep = !prunable<D>(blo, bhi, prec[l], s_ref[ch], dl, s_mr[ch]);
+                }
+                const unsigned long long bal = __ballot(keep);
+                const int k = min(lane, l & 63);   // lanes before this one in its segment
+                if (valid && k == 0) {
+                    const int len = min(64 - lane, min(64 - (l & 63), (int)mp - l));
+                    const unsigned long long seg = (bal >> lane) & (len >= 64 ? ~0ull : ((1ull << len) - 1ull));
+                    if (seg) atomicOr(&cbits[ch * nwc + (l >> 6)], seg << (l & 63));
+                }
+                l += dlp;
+                ch += dch;
+                if (l >= (int)mp) { l -= (int)mp; ++ch; }
+            }
+        }
+        __syncthreads();
+        DBG_T(12);
         // (C)
         for (int p = tid, ch = tid / (int)mp, l = tid % (int)mp; p < npair; p += CAND_TPB) {
-            int f[MAXD];
-            if (child_cell(ch, f)) {
-                const long long cell = encode(f, g.G, D);
+            const long long cell = s_cell[ch];
+            if (cell >= 0) {
                 const unsigned long long *wb = cbits + ch * nwc;
                 const unsigned long long word = wb[l >> 6];
                 uint32_t before = 0;

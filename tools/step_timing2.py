@@ -20,7 +20,7 @@ st = eng.status()
 lib = _lib.load()
 lib.pcm_debug_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
 nb = 8192
-buf = np.zeros((nb, 8), np.uint64)
+buf = np.zeros((nb, 16), np.uint64)
 assert lib.pcm_debug_timing(buf.ctypes.data_as(ctypes.c_void_p), nb) == 0
 t = buf.astype(np.int64)
 nbk = int((t[:, 0] > 0).sum())
@@ -41,3 +41,13 @@ for k0, k1, name in ((6, 4, "coarse reference"), (4, 5, "coarse prune"), (5, 1, 
 print("end of bodies (rel. first start) us: p50 %.1f max %.1f" % (us(np.median(t[:, 3] - t0)), us(t[:, 3].max() - t0)))
 last = t[:, 7].max()
 print("last block finished at %.1f us" % us(last - t0))
+ok = (c[:, 1] > 0) & (c[:, 2] > 0)
+ch = us(c[ok, 2] - c[ok, 1]); mp = c[ok, 8]; bid = np.nonzero(ok)[0]
+o = np.argsort(-ch)[:8]
+print("slowest children blocks (block, us, coarse-list length):", [(int(bid[i]), round(float(ch[i]), 1), int(mp[i])) for i in o])
+print("coarse-list length p10/p50/p90/max:", [int(np.percentile(mp, q)) for q in (10, 50, 90, 100)])
+for k0, k1, name in ((1, 10, "pair 0 (boxes)"), (10, 11, "pair A (refs)"), (11, 12, "pair B (prune)"), (12, 2, "pair C (write)")):
+    ok = (c[:, k0] > 0) & (c[:, k1] > 0)
+    if ok.any():
+        dd = c[ok, k1] - c[ok, k0]
+        print("%s us: p50 %.2f max %.2f (%d blocks)" % (name, us(np.median(dd)), us(dd.max()), ok.sum()))
