@@ -326,7 +326,7 @@ def main():
                        "cells": info["ncells"], "tiles": info["ntiles"], "grid": info["grid"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_lloyd<float,3>",
+                         "kernel": "k_lloyd1<float,3,8>",
                          "algorithmic_bytes_per_point": bytes_pt,
                          "avg_launch_ms": assign_ms, "timing": timing + ("" if world == 1 else " (max over ranks)")},
             "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"]},
