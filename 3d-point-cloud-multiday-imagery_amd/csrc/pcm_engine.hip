@@ -57,6 +57,8 @@ struct pcm_engine {
     uint32_t *perm = nullptr;
     void *lab = nullptr;             // sorted-order labels: uint16 when k <= 65535, else int32
     uint32_t *cell_start = nullptr;
+    uint32_t *sub_start = nullptr;   // [(ncells << d) + 1]: first sorted point of every sub-cell (half-cell per axis)
+    size_t cap_sub = 0;
     uint32_t *tile_off = nullptr;    // [ncells+1] first tile of each cell
     uint4 *tiles = nullptr;
     int num_cu = 256;
@@ -148,11 +150,12 @@ void free_layout(pcm_engine *e) {
 }
 
 void free_buffers(pcm_engine *e) {
-    void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->ws};
+    void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->ws,
+                  e->sub_start};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
-    e->tile_off = nullptr; e->ws = nullptr;
+    e->tile_off = nullptr; e->ws = nullptr; e->sub_start = nullptr; e->cap_sub = 0;
     e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
     e->cap_xs = e->cap_lab = e->cap_perm = e->cap_cells = e->cap_fc = e->cap_tiles = e->cap_ws = 0;
     free_layout(e);
@@ -422,6 +425,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         HIPCHK(ensure(e->fc_cnt, c2, need));
         e->cap_cells = std::min(c0, std::min(c1, c2));
         size_t f0 = e->cap_fc, f1 = e->cap_fc;
+        HIPCHK(ensure(e->sub_start, e->cap_sub, (size_t)((nc << e->d) + 1) * sizeof(uint32_t)));
         HIPCHK(ensure(e->fc_rec, f0, (size_t)nc * CAPF * sizeof(float4)));
         HIPCHK(ensure(e->fc_lab, f1, (size_t)nc * CAPF * sizeof(float4)));   // sized like fc_rec: one capacity
         e->cap_fc = std::min(f0, f1);
@@ -444,8 +448,10 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     }
 
     // scratch arena: keys, sorted keys, values (u32 n each), tile counts (nc), rocprim temp
+    // sort key: cell id << d | sub-cell (which half of the cell per axis)
+    const long long nsub = nc << e->d;
     unsigned bits = 1;
-    while ((1LL << bits) < nc) ++bits;
+    while ((1LL << bits) < nsub) ++bits;
     size_t sort_bytes = 0, scan_bytes = 0;
     if (rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                   (uint32_t *)nullptr, (size_t)n, 0u, bits, s) != hipSuccess ||
@@ -464,7 +470,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
-        k_cellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, keys, vals);
+        k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, keys, vals);
         LAUNCHCHK();
         return 0;
     });
@@ -480,7 +486,9 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         return 0;
     });
     if (rc) return rc;
-    k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, e->cell_start);
+    k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nsub, e->sub_start);
+    LAUNCHCHK();
+    k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, e->d, e->cell_start);
     LAUNCHCHK();
     k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt);
     LAUNCHCHK();
@@ -590,6 +598,8 @@ static LloydArgs lloyd_args(pcm_engine *e) {
     A.partials = e->partials;
     A.pstride = (long long)e->k * (e->d + 1);
     A.ctrl = e->ctrl;
+    A.sub_start = e->sub_start;
+    A.g = e->g;
     return A;
 }
 
@@ -673,8 +683,8 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
                     k_lloyd<TT, D, LS><<<assign_grid(e, (const void *)k_lloyd<TT, D, LS>, lds), TPB, lds, s>>>(
                         A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
                 else
-                    k_lloyd1<TT, D, LS><<<lloyd_grid(e), TPB, lds, s>>>(A, e->tiles, e->fc_rec, e->fc_lab, e->C,
-                                                                          e->fc_cnt);
+                    k_lloyd1<TT, D, LS, (D <= 3 && LS == LSLOT)><<<lloyd_grid(e), TPB, lds, s>>>(
+                        A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
             };
             if (D <= 3 && lloyd_slots(e) == 8) launch(std::integral_constant<int, 8>{});
             else launch(std::integral_constant<int, LSLOT>{});

@@ -241,6 +241,37 @@ __global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long lo
     vals[i] = (uint32_t)i;
 }
 
+// Sort key of the Lloyd layout: the cell id << D | the sub-cell (bit D-1-a set
+// when the point lies in the upper half of its cell along axis a), so that
+// within a cell the points of one sub-cell are contiguous.  The half test uses
+// the same fp64 cell coordinate as the binning (clamped cells: a point on the
+// top face lands in the upper half); sub-cell boxes carry the binning margin on
+// both sides of the split (k_lloyd1).
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_subcellid(const T *__restrict__ X, long long n, Grid g,
+                                                   uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int idx[MAXD];
+    uint32_t sub = 0;
+    for (int a = 0; a < D; ++a) {
+        double t = ((double)to_f<T>(X[i * D + a]) - g.lo[a]) * g.inv[a];
+        int v = (int)floor(t);
+        v = v < 0 ? 0 : (v >= g.G[a] ? g.G[a] - 1 : v);
+        idx[a] = v;
+        sub = (sub << 1) | ((t - (double)v >= 0.5) ? 1u : 0u);
+    }
+    keys[i] = ((uint32_t)encode(idx, g.G, D) << D) | sub;
+    vals[i] = (uint32_t)i;
+}
+
+// cell_start[c] = sub_start[c << d], c in [0, ncells]
+__global__ __launch_bounds__(256) void k_cell_from_sub(const uint32_t *__restrict__ sub_start, long long ncells, int d,
+                                                       uint32_t *__restrict__ cell_start) {
+    long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (c <= ncells) cell_start[c] = sub_start[c << d];
+}
+
 // Sorted point layout "AoSoA-4": the points in cell order, in groups of 4
 // consecutive points stored coordinate-major -- [x0 x1 x2 x3][y0 .. y3][z0 .. z3]
 // -- so one lane's 4 points arrive from b128 loads already paired for the
@@ -781,6 +812,30 @@ __device__ __forceinline__ void scan4(P rec, int mm, const float (&x)[4][D], flo
     }
 }
 
+// Same scan over the list positions set in a wave-uniform mask (ascending, so
+// the lowest index still wins ties); m has at least one bit set.
+template <int D, typename P>
+__device__ __forceinline__ void scan4_m(P rec, unsigned long long m, const float (&x)[4][D], float (&bd)[4],
+                                        int (&bj)[4]) {
+    {
+        const int j = __builtin_ctzll(m);
+        m &= m - 1ull;
+        const float4 c = rec[j];
+        for (int e = 0; e < 4; ++e) { bd[e] = dist_canon<D>(x[e], c); bj[e] = j; }
+    }
+    while (m) {
+        const int j = __builtin_ctzll(m);
+        m &= m - 1ull;
+        const float4 c = rec[j];
+        for (int e = 0; e < 4; ++e) {
+            float dd = dist_canon<D>(x[e], c);
+            bool lt = dd < bd[e];
+            bd[e] = lt ? dd : bd[e];
+            bj[e] = lt ? j : bj[e];
+        }
+    }
+}
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -899,6 +954,8 @@ struct LloydArgs {
     unsigned long long *partials;   // accumulation target: + (iter & 1) * pstride
     long long pstride;              // K*(D+1): single-GPU parity halves; 0: the all-reduce buffer itself
     const Ctrl *ctrl;
+    const uint32_t *sub_start;      // [(ncells << D) + 1] sub-cell starts (k_lloyd1's per-round candidate masks)
+    Grid g;
 };
 
 struct TileL {
@@ -1295,7 +1352,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
 // a quarter of its lifetime at config 3).  The list loads precede the point
 // loads, so the in-order vmcnt wait for the first work item covers them.
 constexpr int LSPEC = 16;   // list records loaded before the count is known
-template <typename T, int D, int LS>
+#ifndef PCM_MASK_MIN
+#define PCM_MASK_MIN 2
+#endif
+constexpr int MASK_MIN = PCM_MASK_MIN;   // sub-cell masks for lists of at least this length
+template <typename T, int D, int LS, bool MASK>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8))) void k_lloyd1(
     LloydArgs A, const uint4 *__restrict__ tiles, const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
     const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt) {
@@ -1325,6 +1386,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         l0 = fc_lab[(size_t)cell * CAPF + tid];
     }
     const uint32_t cnt = fc_cnt[cell];
+    constexpr int NSUB = 1 << D;
+    uint32_t ss[NSUB + 1];   // the cell's sub-cell starts (uniform: scalar loads)
+#pragma unroll
+    for (int o = 0; o <= NSUB; ++o) ss[o] = A.sub_start[((size_t)cell << D) + o];
     const unsigned base0 = start & ~3u;
     const int nr = (int)((end - base0 + 4 * TPB - 1) / (4 * TPB));
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
@@ -1356,7 +1421,85 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     uint32_t *const myacc = acc + (tid & (AW - 1));
     unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.pstride;
     __syncthreads();
+    // Sub-cell candidate masks: for every half-cell box (one per axis
+    // combination) the list positions its reference does not dominate (the
+    // exact test of the candidate lists, at the current centres), then per
+    // round the union over the sub-cells the round's points occupy.  Points are
+    // sorted by sub-cell within the cell, so a round (512 points) spans one or
+    // two sub-cells and scans ~the candidates of a cell half as wide; any
+    // superset of the undominated candidates, scanned in ascending order, gives
+    // the exact labels (a dominated candidate is strictly farther for every
+    // point of the box, so every tied minimiser is kept).
+    __shared__ unsigned long long omask[NSUB];
+    __shared__ uint32_t okey[NSUB];
+    __shared__ unsigned long long rmask[16];   // rounds of one tile: <= TILE / (4 TPB) + 1
+    // only coarse grids (MASK: the 16-slot D <= 3 variant, lists of ~6 at a
+    // 12.5M shard: 47.8 -> 43.5 us per launch); at config 3 (lists of ~2.7)
+    // and D = 4 (16 sub-cells) the mask phase at the block's start cost more
+    // than the shorter scans saved (217 -> 225 us, 415 -> 488 us)
+    const bool use_mask = MASK && !full && mm >= MASK_MIN && A.g.prune;
+    if (use_mask) {
+        int ci[MAXD];
+        for (int a = D - 1, c = (int)cell; a >= 0; --a) {   // cell ids fit 32 bits (sort keys)
+            ci[a] = (int)((unsigned)c % (unsigned)A.g.G[a]);
+            c = (int)((unsigned)c / (unsigned)A.g.G[a]);
+        }
+        double cblo[MAXD], cbhi[MAXD], mid[MAXD];
+        cell_box<D>(A.g, ci, ci, cblo, cbhi);
+#pragma unroll
+        for (int a = 0; a < D; ++a) mid[a] = A.g.lo[a] + ((double)ci[a] + 0.5) * A.g.w[a];
+        auto sub_box = [&](int o, double *blo, double *bhi) {
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                const bool up = (o >> (D - 1 - a)) & 1;
+                blo[a] = up ? mid[a] - A.g.mg[a] : cblo[a];
+                bhi[a] = up ? cbhi[a] : mid[a] + A.g.mg[a];
+            }
+        };
+        if (tid < NSUB) { okey[tid] = ~0u; omask[tid] = 0ull; }
+        __syncthreads();
+        // (sub-cell o, list position j) pairs: reference = a candidate nearest
+        // the sub-cell's centre (LDS atomic min of the key of k_step's children)
+        const int np = NSUB * mm;
+        for (int p = tid; p < np; p += TPB) {
+            const int o = p / mm, j = p - o * mm;
+            double blo[MAXD], bhi[MAXD];
+            sub_box(o, blo, bhi);
+            const float4 c = crec[j];
+            float dsum = 0.f;
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                const float dd = (float)(0.5 * (blo[a] + bhi[a])) - comp(c, a);
+                dsum += dd * dd;
+            }
+            atomicMin(&okey[o], (__float_as_uint(dsum) & ~0x3Fu) | (uint32_t)j);
+        }
+        __syncthreads();
+        for (int p = tid; p < np; p += TPB) {
+            const int o = p / mm, j = p - o * mm;
+            double blo[MAXD], bhi[MAXD];
+            sub_box(o, blo, bhi);
+            uint32_t bl = okey[o] & 0x3Fu;
+            if (bl >= (uint32_t)mm) bl = 0;
+            if (!prunable<D>(blo, bhi, crec[j], crec[bl])) atomicOr(&omask[o], 1ull << j);
+        }
+        __syncthreads();
+        if (tid < nr) {
+            const unsigned rb = base0 + (unsigned)tid * 4u * TPB;
+            const unsigned rbeg = rb > start ? rb : start;
+            const unsigned rend = rb + 4u * TPB < end ? rb + 4u * TPB : end;
+            unsigned long long m = 0ull;
+#pragma unroll
+            for (int o = 0; o < NSUB; ++o)
+                if (ss[o] < rend && ss[o + 1] > rbeg) m |= omask[o];
+            rmask[tid] = m;
+        }
+        __syncthreads();
+    }
     DBG_L(1);
+#ifdef PCM_ABL_NOACC
+    int abl_sink = 0;
+#endif
 
     // loads per work item; after item r+2's are issued, items r+1 and r+2 may
     // stay outstanding while r is computed
@@ -1384,6 +1527,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         if (mm == 1) {
 #endif
             for (int e = 0; e < 4; ++e) bj[e] = 0;
+        } else if (use_mask) {
+            const unsigned long long m0 = rmask[r];
+            const unsigned long long m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(m0 >> 32)) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m0);
+            if ((m & (m - 1ull)) == 0ull) {   // one candidate for the whole round
+                const int j = m ? __builtin_ctzll(m) : 0;
+                for (int e = 0; e < 4; ++e) bj[e] = j;
+            } else {
+                float bd[4];
+                scan4_m<D>(crec, m, x, bd, bj);
+            }
         } else {
             float bd[4];
             if (full) scan4_s<D>(Call, mm, x, bd, bj);
@@ -1399,11 +1553,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
             over |= v && hi;
             sl[e] = (v && !hi) ? bj[e] : LS;
         }
+#ifdef PCM_ABL_NOACC
+        for (int e = 0; e < 4; ++e)
+            for (int a = 0; a < D; ++a) abl_sink += fixed_i(x[e][a], A.q[a]) + sl[e];
+        over = false;
+#else
         for (int e = 0; e < 4; ++e) {
             uint32_t *ap = myacc + sl[e] * ((D + 1) * AW);
             for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
             atomicAdd(ap + D * AW, 1u);
         }
+#endif
         if (over) {   // list positions >= LS (long lists only)
             for (int e = 0; e < 4; ++e) {
                 const bool v = whole || ((i0 + e >= start) && (i0 + e < end));
@@ -1432,6 +1592,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         step(xc, xb, r + 2);
     }
     DBG_L(2);
+#ifdef PCM_ABL_NOACC
+    if (abl_sink == 0x7fffffff) acc[0] = 1u;
+#endif
     // fold the slot words into the int64 statistics: 16 threads per (slot, a) row
     __syncthreads();
     {
