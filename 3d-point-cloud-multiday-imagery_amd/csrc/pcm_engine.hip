@@ -58,6 +58,7 @@ struct pcm_engine {
     void *lab = nullptr;             // sorted-order labels: uint16 when k <= 65535, else int32
     uint32_t *cell_start = nullptr;
     uint32_t *sub_start = nullptr;   // [(ncells << d) + 1]: first sorted point of every sub-cell (half-cell per axis)
+    int sub = 0;                     // the current layout is sorted by sub-cell
     size_t cap_sub = 0;
     uint32_t *tile_off = nullptr;    // [ncells+1] first tile of each cell
     uint4 *tiles = nullptr;
@@ -390,6 +391,8 @@ int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream, doubl
     return 0;
 }
 
+static int lloyd_slots(const pcm_engine *e);
+
 int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gidx0, void *stream) {
     if (!e || !q) return fail(PCM_E_ARG, "bad argument");
     if (!e->have_bbox) return fail(PCM_E_STATE, "pcm_layout_bbox must run first");
@@ -448,8 +451,12 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     }
 
     // scratch arena: keys, sorted keys, values (u32 n each), tile counts (nc), rocprim temp
-    // sort key: cell id << d | sub-cell (which half of the cell per axis)
-    const long long nsub = nc << e->d;
+    // sort key: cell id << d | sub-cell (which half of the cell per axis) on the
+    // coarse grids whose k_lloyd1 variant uses sub-cell masks (the 16-slot D <= 3
+    // one, see lloyd_slots); else the cell id (one radix pass fewer at config 3)
+    e->sub = (e->d <= 3 && lloyd_slots(e) == LSLOT) ? 1 : 0;
+    const int sh = e->sub ? e->d : 0;
+    const long long nsub = nc << sh;
     unsigned bits = 1;
     while ((1LL << bits) < nsub) ++bits;
     size_t sort_bytes = 0, scan_bytes = 0;
@@ -470,7 +477,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
-        k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, keys, vals);
+        k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, keys, vals);
         LAUNCHCHK();
         return 0;
     });
@@ -488,7 +495,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     if (rc) return rc;
     k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nsub, e->sub_start);
     LAUNCHCHK();
-    k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, e->d, e->cell_start);
+    k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, sh, e->cell_start);
     LAUNCHCHK();
     k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt);
     LAUNCHCHK();
@@ -599,6 +606,7 @@ static LloydArgs lloyd_args(pcm_engine *e) {
     A.pstride = (long long)e->k * (e->d + 1);
     A.ctrl = e->ctrl;
     A.sub_start = e->sub_start;
+    A.sub = e->sub;
     A.g = e->g;
     return A;
 }

@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long lo
 // top face lands in the upper half); sub-cell boxes carry the binning margin on
 // both sides of the split (k_lloyd1).
 template <typename T, int D>
-__global__ __launch_bounds__(256) void k_subcellid(const T *__restrict__ X, long long n, Grid g,
+__global__ __launch_bounds__(256) void k_subcellid(const T *__restrict__ X, long long n, Grid g, int with_sub,
                                                    uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void k_subcellid(const T *__restrict__ X, long
         idx[a] = v;
         sub = (sub << 1) | ((t - (double)v >= 0.5) ? 1u : 0u);
     }
-    keys[i] = ((uint32_t)encode(idx, g.G, D) << D) | sub;
+    keys[i] = with_sub ? ((uint32_t)encode(idx, g.G, D) << D) | sub : (uint32_t)encode(idx, g.G, D);
     vals[i] = (uint32_t)i;
 }
 
@@ -955,6 +955,7 @@ struct LloydArgs {
     long long pstride;              // K*(D+1): single-GPU parity halves; 0: the all-reduce buffer itself
     const Ctrl *ctrl;
     const uint32_t *sub_start;      // [(ncells << D) + 1] sub-cell starts (k_lloyd1's per-round candidate masks)
+    int sub;                        // the layout is sorted by sub-cell (else sub_start is [ncells + 1])
     Grid g;
 };
 
@@ -1389,7 +1390,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     constexpr int NSUB = 1 << D;
     uint32_t ss[NSUB + 1];   // the cell's sub-cell starts (uniform: scalar loads)
 #pragma unroll
-    for (int o = 0; o <= NSUB; ++o) ss[o] = A.sub_start[((size_t)cell << D) + o];
+    for (int o = 0; o <= NSUB; ++o) ss[o] = (MASK && A.sub) ? A.sub_start[((size_t)cell << D) + o] : 0u;
     const unsigned base0 = start & ~3u;
     const int nr = (int)((end - base0 + 4 * TPB - 1) / (4 * TPB));
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
@@ -1437,7 +1438,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     // 12.5M shard: 47.8 -> 43.5 us per launch); at config 3 (lists of ~2.7)
     // and D = 4 (16 sub-cells) the mask phase at the block's start cost more
     // than the shorter scans saved (217 -> 225 us, 415 -> 488 us)
-    const bool use_mask = MASK && !full && mm >= MASK_MIN && A.g.prune;
+    const bool use_mask = MASK && A.sub && !full && mm >= MASK_MIN && A.g.prune;
     if (use_mask) {
         int ci[MAXD];
         for (int a = D - 1, c = (int)cell; a >= 0; --a) {   // cell ids fit 32 bits (sort keys)
