@@ -1361,7 +1361,6 @@ template <typename T, int D, int LS, bool MASK>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8))) void k_lloyd1(
     LloydArgs A, const uint4 *__restrict__ tiles, const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
     const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt) {
-    if (gated(A.ctrl)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LS+1)*(D+1)][AW]
     __shared__ float4 crec[CAPF];
     __shared__ int32_t cid[CAPF];
@@ -1373,11 +1372,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
     const int tid = threadIdx.x;
     const unsigned t = blockIdx.x;
-    // the tiles buffer holds ntiles_cap >= gridDim.x records: the load is in
-    // bounds before the device tile count says whether this block has work
-    const uint4 tr = tiles[t];
-    const unsigned nt = *A.ntiles;
-    if (t >= nt) return;
+    // the gate flags, the device tile count and the tile record are loaded
+    // together (one memory latency, not three in a row): the tiles buffer holds
+    // ntiles_cap >= gridDim.x records, so the record load is in bounds before
+    // the count says whether this block has work
+    uint4 tr = tiles[t];
+    unsigned nt = *A.ntiles;
+    unsigned gate = A.ctrl->halt | A.ctrl->done;
+    asm volatile("" : "+s"(tr.x), "+s"(tr.y), "+s"(tr.z), "+s"(nt), "+s"(gate));   // keep the loads above the exits
+    if (gate != 0u || t >= nt) return;
     DBG_L(0);
     const unsigned cell = tr.x, start = tr.y, end = tr.z;
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1846,7 +1849,13 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
                                               int32_t *__restrict__ fc_lab, int bpc, double alpha, double dl_cap) {
     static_assert(1024 % CAND_TPB == 0 && CAND_TPB >= 128, "shift tree: 1024 lanes over the block");
     constexpr int NU = 1024 / CAND_TPB;   // shift-tree lanes L = tid + CAND_TPB * u per thread
-    if (gated(ctrl)) return;
+    // the gate flags and the control words this launch reads, in one memory latency
+    unsigned gate = ctrl->halt | ctrl->done;
+    unsigned par = ctrl->iter & 1u;
+    unsigned sel = ctrl->ref_sel;
+    double budget = ctrl->budget;
+    asm volatile("" : "+s"(gate), "+s"(par), "+s"(sel), "+s"(budget));   // keep the loads above the exit
+    if (gate != 0u) return;
     DBG_T(0);
     extern __shared__ __attribute__((aligned(16))) float4 cn[];   // [K]
     __shared__ unsigned s_empty, s_last;
@@ -1855,9 +1864,6 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
     __shared__ double s_dmax[CAND_TPB / 64], s_smax[CAND_TPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = K * (D + 1);
-    const unsigned par = ctrl->iter & 1u;
-    const unsigned sel = ctrl->ref_sel;
-    const double budget = ctrl->budget;
     const unsigned long long *src = stats_in ? stats_in : partials + (size_t)par * n;
     const float4 *ref = cref + (size_t)sel * K;
     if (tid == 0) { s_empty = 0; s_neq = 0ull; }
@@ -2188,6 +2194,30 @@ __global__ __launch_bounds__(256) void k_unpermute(const LT *__restrict__ lab, c
                                                    long long n, int32_t *__restrict__ out) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i < n) out[perm ? perm[i] : (uint32_t)i] = (int32_t)lab[i];
+}
+
+// Scatter of the sorted-order labels into row order restricted to the rows
+// [r0, r1) (destination windows small enough to stay in the Infinity Cache
+// while the random writes land: partial lines merge on-die instead of each
+// 2-4 B write costing an HBM burst).
+template <typename LT, typename OT>
+__global__ __launch_bounds__(256) void k_unpermute_win(const LT *__restrict__ lab, const uint32_t *__restrict__ perm,
+                                                       long long n, uint32_t r0, uint32_t r1, OT *__restrict__ out) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = perm[i];
+    if (r >= r0 && r < r1) out[r] = (OT)lab[i];
+}
+
+// uint16 row-order labels -> int32 (0xffff stays -1 only where K > 65535, which never takes this path)
+__global__ __launch_bounds__(256) void k_widen_u16(const uint16_t *__restrict__ in, long long n, int32_t *__restrict__ out) {
+    long long i = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * 4;
+    if (i + 4 <= n) {
+        const uint2 w = *reinterpret_cast<const uint2 *>(in + i);
+        *reinterpret_cast<int4 *>(out + i) = make_int4((int)(w.x & 0xffffu), (int)(w.x >> 16), (int)(w.y & 0xffffu), (int)(w.y >> 16));
+    } else {
+        for (; i < n; ++i) out[i] = (int32_t)in[i];
+    }
 }
 
 template <int D>

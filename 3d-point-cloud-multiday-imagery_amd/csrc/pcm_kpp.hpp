@@ -38,6 +38,7 @@ constexpr int KPP_OB = 1 << KPP_OB_LOG;
 constexpr int KPP_CELL_PTS = 256;              // target points per pruning cell
 constexpr int KPP_STPB = 1024;                 // k_kpp_search block size
 constexpr int KPP_RED_BLOCKS = 64;             // gmax reduction blocks of k_kpp_search
+constexpr int KPP_SCU = 32;                    // k_kpp_search: 64-wide chunks of block sums kept in registers per wave
 
 struct KppCtl {
     float4 cand[KPP_LMAX];
@@ -127,6 +128,28 @@ __device__ __forceinline__ float wave_max_f(float v) {
     return v;
 }
 
+// Visit the points [b, e) of one cell with a wave, 4 points per lane per pass:
+// the coordinate and `closest` loads of the 4 points are all issued before any
+// is used (a cell holds ~KPP_CELL_PTS = 256 points: one pass, one memory
+// latency, instead of four dependent rounds).  f(i, x, closest_i) per point.
+template <int D, typename F>
+__device__ __forceinline__ void kpp_cell_points(const float *__restrict__ xs, const float *__restrict__ closest,
+                                                uint32_t b, uint32_t e, int lane, F &&f) {
+    for (uint32_t i0 = b + lane; i0 < e; i0 += 256) {
+        float x[4][D], cl[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + 64u * u;
+            const uint32_t ii = i < e ? i : i0;
+            kpp_point<D>(xs, ii, x[u]);
+            cl[u] = closest[ii];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i0 + 64u * u < e) f(i0 + 64u * u, x[u], cl[u]);
+    }
+}
+
 // Step 0: closest := d(x, c0) for every point, cell maxima, original-order
 // block sums of the weights and the potential.  One wave per cell (strided).
 template <int D>
@@ -184,6 +207,17 @@ __device__ __forceinline__ unsigned long long kpp_block_exscan(unsigned long lon
 }
 
 // Step c (>= 1): blocks t < L locate candidate t; blocks >= L reduce gmax.
+//  1. the original-order weight block holding target tg: wave w owns a
+//     contiguous segment of the block sums and reads it coalesced (lane l,
+//     chunk u: sum index seg + 64 u + l), KPP_SCU chunks kept in registers; the
+//     wave totals give each segment's exclusive base, and the one wave whose
+//     segment holds the target scans its chunks (wave prefix sums) for the
+//     unique block with  incl >= tg  and  (first block or excl < tg);
+//  2. the same unique-row test inside that block (4096 rows, 4 per thread,
+//     a block prefix scan): a plain LDS store, no atomic.
+// Measured per-phase (tools/kpp_timing.py): per-thread ranges of 24 sums
+// (uncoalesced, one latency each) and an LDS atomicMin of every row past the
+// target made this launch 45-54 us per centre.
 template <int D>
 __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long long *__restrict__ bsum, long long nb,
                                                          const float *__restrict__ closest,
@@ -191,7 +225,8 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
                                                          long long n, const unsigned long long *__restrict__ umant,
                                                          int L, int s, int c, const float *__restrict__ cmax,
                                                          long long ncells, KppCtl *__restrict__ ctl) {
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    DBG_T(0);
     if ((int)blockIdx.x >= L) {   // gmax: max over the cells' max closest
         unsigned int m = 0u;
         for (long long cl = (blockIdx.x - L) * (long long)KPP_STPB + tid; cl < ncells;
@@ -199,35 +234,81 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
             m = max(m, __float_as_uint(cmax[cl]));
         for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o));
         if (lane == 0 && m) atomicMax(&ctl->gmax_acc[c & 1], m);
+        DBG_T(8);
         return;
     }
     const int t = blockIdx.x;
     if (t == 0)
         for (int l = tid; l < KPP_LMAX; l += KPP_STPB) ctl->delta[l] = 0ull;
-    __shared__ unsigned long long wtot[KPP_STPB / 64];
+    constexpr int NWV = KPP_STPB / 64;
+    __shared__ unsigned long long wtot[NWV];
     __shared__ long long s_blk;
     __shared__ unsigned long long s_res;
     __shared__ long long s_found;
     const unsigned long long pot = ctl->pot[c & 1];
     const unsigned long long m = umant[t];
+    if (tid == 0) { s_blk = -1; s_found = 0x7fffffffffffffffll; }
+    // 1. this wave's segment [sb, se) of the block sums, 64-wide chunks (issued
+    // before the target is computed: the loads do not wait for pot / umant)
+    const long long seg = ((nb + NWV * 64 - 1) / (NWV * 64)) * 64;
+    const long long sb = min((long long)wv * seg, nb), se = min(sb + seg, nb);
+    const int nch = (int)((se - sb + 63) / 64);
+    constexpr int CU = KPP_SCU;
+    unsigned long long v[CU];
+    unsigned long long lsum = 0ull;
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+        const long long b = sb + 64LL * u + lane;
+        v[u] = (u < nch && b < se) ? bsum[b] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < CU; ++u) lsum += v[u];
+    for (int u = CU; u < nch; ++u) {   // segments longer than the register cache (n > ~134M points)
+        const long long b = sb + 64LL * u + lane;
+        lsum += b < se ? bsum[b] : 0ull;
+    }
     const unsigned long long lo = m * pot, hi = __umul64hi(m, pot);
     const unsigned long long tg = (hi << 11) | (lo >> 53);   // floor(u * pot), u = m / 2^53
-    if (tid == 0) { s_blk = -1; s_found = 0x7fffffffffffffffll; }
-    // 1. original-order block containing the target: thread tid owns blocks [b0, b1)
-    const long long per = (nb + KPP_STPB - 1) / KPP_STPB;
-    const long long b0 = min((long long)tid * per, nb), b1 = min(b0 + per, nb);
-    unsigned long long loc = 0ull;
-    for (long long b = b0; b < b1; ++b) loc += bsum[b];
-    unsigned long long r = kpp_block_exscan(loc, wtot);   // exclusive prefix of this thread's range
-    for (long long b = b0; b < b1; ++b) {
-        const unsigned long long v = bsum[b];
-        if (r + v >= tg && (b == 0 || r < tg)) {   // first block whose inclusive prefix reaches tg
-            s_blk = b;
-            s_res = tg - r;
+    const unsigned long long wsum = wave_sum_u64(lsum);
+    if (lane == 0) wtot[wv] = wsum;
+    __syncthreads();
+    DBG_T(2);
+    unsigned long long base = 0ull;
+    for (int w = 0; w < wv; ++w) base += wtot[w];
+    const bool mine = (tg == 0ull) ? (sb == 0 && se > 0) : (base < tg && tg <= base + wsum);
+    if (mine) {   // wave-uniform
+        // the chunk holding the target from the chunk totals (register chunks:
+        // static indices), then one wave prefix scan of that chunk
+        unsigned long long r = base, x = 0ull;
+        int uc = -1;
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            const unsigned long long ct = wave_sum_u64(v[u]);
+            if (uc < 0 && u < nch && (r + ct >= tg)) { uc = u; x = v[u]; }
+            if (uc < 0) r += ct;
         }
-        r += v;
+        for (int u = CU; uc < 0 && u < nch; ++u) {   // past the register cache (n > ~134M points)
+            const long long b = sb + 64LL * u + lane;
+            const unsigned long long y = b < se ? bsum[b] : 0ull;
+            const unsigned long long ct = wave_sum_u64(y);
+            if (r + ct >= tg) { uc = u; x = y; } else { r += ct; }
+        }
+        if (uc >= 0) {
+            const long long b = sb + 64LL * uc + lane;
+            unsigned long long inc = x;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned long long y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
+            }
+            const unsigned long long ex = r + inc - x;
+            if (b < se && r + inc >= tg && (b == 0 || ex < tg)) {   // first block whose inclusive prefix reaches tg
+                s_blk = b;
+                s_res = tg - ex;
+            }
+        }
     }
     __syncthreads();
+    DBG_T(4);
     const long long blk = s_blk;
     long long idx = n - 1;   // past the end (np.searchsorted -> n, clipped): not reachable, tg < pot
     if (blk >= 0) {
@@ -236,29 +317,38 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
         constexpr int PER = KPP_OB / KPP_STPB;
         unsigned long long w[PER];
         unsigned long long l2 = 0ull;
+        uint32_t ir[PER];
 #pragma unroll
         for (int e = 0; e < PER; ++e) {
             const long long j = blk * KPP_OB + (long long)tid * PER + e;
-            w[e] = j < n ? kpp_w(closest[inv[j]], s) : 0ull;
+            ir[e] = j < n ? inv[j] : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+            const long long j = blk * KPP_OB + (long long)tid * PER + e;
+            w[e] = j < n ? kpp_w(closest[ir[e]], s) : 0ull;
             l2 += w[e];
         }
+        DBG_T(5);
         unsigned long long q = kpp_block_exscan(l2, wtot);
 #pragma unroll
         for (int e = 0; e < PER; ++e) {
             const long long j = blk * KPP_OB + (long long)tid * PER + e;
-            if (j < n && q + w[e] >= rs) atomicMin(&s_found, j);
+            if (j < n && q + w[e] >= rs && (j == blk * KPP_OB || q < rs)) s_found = j;   // unique row
             q += w[e];
         }
         __syncthreads();
         idx = s_found < n ? s_found : n - 1;
     }
+    DBG_T(6);
     if (tid == 0) {
-        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        float vv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int a = 0; a < D; ++a) v[a] = X[idx * D + a];
-        ctl->cand[t] = make_float4(v[0], v[1], v[2], v[3]);
+        for (int a = 0; a < D; ++a) vv[a] = X[idx * D + a];
+        ctl->cand[t] = make_float4(vv[0], vv[1], vv[2], vv[3]);
         ctl->cand_idx[t] = idx;
     }
+    DBG_T(7);
 }
 
 // Step c: potential drop of every candidate over the cells it reaches.  While
@@ -306,10 +396,7 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
             const unsigned mask = (unsigned)__ballot(reach);
             if (!mask) continue;   // wave-uniform
             const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
-            for (uint32_t i = b + lane; i < e; i += 64) {
-                float x[D];
-                kpp_point<D>(xs, i, x);
-                const float cl = closest[i];
+            kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t, const float (&x)[D], float cl) {
                 const unsigned long long wcl = kpp_w(cl, s);
 #pragma unroll
                 for (int q = 0; q < KPP_LMAX; ++q) {
@@ -317,30 +404,47 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
                     const float d = dist_canon<D>(x, s_cand[q]);
                     if (d < cl) dw[q] += wcl - kpp_w(d, s);
                 }
-            }
+            });
         }
     } else {
-        int l = 0;
-        for (long long it = wid; it < total; it += nw) {
-            while (it >= s_off[l + 1]) ++l;   // items ascend per wave
-            int i0[MAXD], i1[MAXD];
+        // this wave's items wid, wid + nw, ... (ipw of them): their reach tests
+        // run one per lane (cmax and the cell bounds of up to 64 items loaded
+        // together: one memory latency), then the reached cells one after
+        // another (wave-uniform)
+        const long long ipw = total > wid ? (total - wid + nw - 1) / nw : 0;
+        for (long long k0 = 0; k0 < ipw; k0 += 64) {
+            const long long it = wid + (k0 + lane) * nw;
+            long long cell = 0;
+            bool reach = false;
+            uint32_t cb = 0u, ce = 0u;
+            int l = 0;
+            if (k0 + lane < ipw) {
+                while (it >= s_off[l + 1]) ++l;
+                int i0[MAXD], i1[MAXD];
 #pragma unroll
-            for (int a = 0; a < D; ++a) { i0[a] = s_i0[l][a]; i1[a] = s_i1[l][a]; }
-            const long long cell = kpp_cube_cell<D>(g, i0, i1, it - s_off[l]);
-            const float4 cd = s_cand[l];
-            if (!kpp_reaches<D>(g, cell, cd, cmax[cell])) continue;   // wave-uniform
-            const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
-            unsigned long long v = 0ull;
-            for (uint32_t i = b + lane; i < e; i += 64) {
-                float x[D];
-                kpp_point<D>(xs, i, x);
-                const float d = dist_canon<D>(x, cd);
-                const float cl = closest[i];
-                if (d < cl) v += kpp_w(cl, s) - kpp_w(d, s);
+                for (int a = 0; a < D; ++a) { i0[a] = s_i0[l][a]; i1[a] = s_i1[l][a]; }
+                cell = kpp_cube_cell<D>(g, i0, i1, it - s_off[l]);
+                const float cm = cmax[cell];
+                cb = cell_start[cell];
+                ce = cell_start[cell + 1];
+                reach = kpp_reaches<D>(g, cell, s_cand[l], cm);
             }
+            unsigned long long bits = __ballot(reach);
+            while (bits) {
+                const int src = __builtin_ctzll(bits);
+                bits &= bits - 1ull;
+                const int lq = __shfl(l, src);
+                const uint32_t b = (uint32_t)__shfl((int)cb, src), e = (uint32_t)__shfl((int)ce, src);
+                const float4 cd = s_cand[lq];
+                unsigned long long v = 0ull;
+                kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t, const float (&x)[D], float cl) {
+                    const float d = dist_canon<D>(x, cd);
+                    if (d < cl) v += kpp_w(cl, s) - kpp_w(d, s);
+                });
 #pragma unroll
-            for (int q = 0; q < KPP_LMAX; ++q)
-                if (q == l) dw[q] += v;
+                for (int q = 0; q < KPP_LMAX; ++q)
+                    if (q == lq) dw[q] += v;
+            }
         }
     }
 #pragma unroll
@@ -381,24 +485,39 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
     kpp_cube<D>(g, best, gmax, i0, i1, vol);
     const long long wid = (blockIdx.x * (long long)blockDim.x + tid) >> 6;
     const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-    for (long long it = wid; it < vol; it += nw) {
-        const long long cell = kpp_cube_cell<D>(g, i0, i1, it);
-        if (!kpp_reaches<D>(g, cell, best, cmax[cell])) continue;   // wave-uniform
-        const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
-        float mx = 0.f;
-        for (uint32_t i = b + lane; i < e; i += 64) {
-            float x[D];
-            kpp_point<D>(xs, i, x);
-            const float d = dist_canon<D>(x, best);
-            const float cl = closest[i];
-            if (d < cl) {
-                closest[i] = d;
-                atomicAdd(&bsum[perm[i] >> KPP_OB_LOG], ~(kpp_w(cl, s) - kpp_w(d, s)) + 1ull);   // -= (mod 2^64)
-            }
-            mx = fmaxf(mx, fminf(d, cl));
+    // this wave's cube cells wid, wid + nw, ...: reach tests one per lane (one
+    // memory latency for up to 64), then the reached cells one after another
+    const long long ipw = vol > wid ? (vol - wid + nw - 1) / nw : 0;
+    for (long long k0 = 0; k0 < ipw; k0 += 64) {
+        const long long itl = wid + (k0 + lane) * nw;
+        long long celll = 0;
+        bool reach = false;
+        uint32_t cbl = 0u, cel = 0u;
+        if (k0 + lane < ipw) {
+            celll = kpp_cube_cell<D>(g, i0, i1, itl);
+            const float cm = cmax[celll];
+            cbl = cell_start[celll];
+            cel = cell_start[celll + 1];
+            reach = kpp_reaches<D>(g, celll, best, cm);
         }
-        mx = wave_max_f(mx);
-        if (lane == 0) cmax[cell] = mx;
+        unsigned long long bits = __ballot(reach);
+        while (bits) {
+            const int src = __builtin_ctzll(bits);
+            bits &= bits - 1ull;
+            const long long cell = (long long)__shfl((int)celll, src);   // cell ids < 2^31 (kpp grid <= 2^20 cells)
+            const uint32_t b = (uint32_t)__shfl((int)cbl, src), e = (uint32_t)__shfl((int)cel, src);
+            float mx = 0.f;
+            kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t i, const float (&x)[D], float cl) {
+                const float d = dist_canon<D>(x, best);
+                if (d < cl) {
+                    closest[i] = d;
+                    atomicAdd(&bsum[perm[i] >> KPP_OB_LOG], ~(kpp_w(cl, s) - kpp_w(d, s)) + 1ull);   // -= (mod 2^64)
+                }
+                mx = fmaxf(mx, fminf(d, cl));
+            });
+            mx = wave_max_f(mx);
+            if (lane == 0) cmax[cell] = mx;
+        }
     }
 }
 
