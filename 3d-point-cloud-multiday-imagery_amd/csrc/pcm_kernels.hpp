@@ -450,8 +450,14 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         const float4 r = C[(int)min((unsigned long long)(K - 1), rkey & 0xFFFFFFFFull)];
         const double mr = dl > 0.0 ? sqrt(maxdist<D>(blo, bhi, r)) : 0.0;
         if (bitmap) {
-            for (int j = tid; j < K; j += CAND_TPB)
-                if (!prunable<D>(blo, bhi, C[j], r, dl, mr)) atomicOr(&kbits[j >> 6], 1ull << (j & 63));
+            // a wave's 64 consecutive centres fill one bitmap word: a ballot and a
+            // plain store (no 64-way contended LDS atomic)
+            for (int j0 = 0; j0 < K; j0 += CAND_TPB) {
+                const int j = j0 + tid;
+                const bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r, dl, mr);
+                const unsigned long long bal = __ballot(keep);
+                if (lane == 0 && j0 + wv * 64 < K) kbits[(j0 >> 6) + wv] = bal;
+            }
             __syncthreads();
             DBG_T(5);
             // ordered compaction: word prefix counts by one wave-wide scan, then

@@ -390,21 +390,37 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
 #pragma unroll
     for (int q = 0; q < KPP_LMAX; ++q) dw[q] = 0ull;
     if (total > g.ncells) {
-        for (long long cell = wid; cell < g.ncells; cell += nw) {
-            const float cm = cmax[cell];
-            const bool reach = lane < L && kpp_reaches<D>(g, cell, s_cand[lane < L ? lane : 0], cm);
-            const unsigned mask = (unsigned)__ballot(reach);
-            if (!mask) continue;   // wave-uniform
-            const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
-            kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t, const float (&x)[D], float cl) {
-                const unsigned long long wcl = kpp_w(cl, s);
+        // this wave's cells wid, wid + nw, ...: one per lane, each lane tests its
+        // cell against every candidate (cmax and the bounds of up to 64 cells
+        // loaded together), then the reached cells one after another
+        const long long cpw = g.ncells > wid ? (g.ncells - wid + nw - 1) / nw : 0;
+        for (long long k0 = 0; k0 < cpw; k0 += 64) {
+            unsigned lmask = 0u;
+            uint32_t cb = 0u, ce = 0u;
+            if (k0 + lane < cpw) {
+                const long long cl = wid + (k0 + lane) * nw;
+                const float cm = cmax[cl];
+                cb = cell_start[cl];
+                ce = cell_start[cl + 1];
+                for (int q = 0; q < L; ++q)
+                    if (kpp_reaches<D>(g, cl, s_cand[q], cm)) lmask |= 1u << q;
+            }
+            unsigned long long bits = __ballot(lmask != 0u);
+            while (bits) {
+                const int src = __builtin_ctzll(bits);
+                bits &= bits - 1ull;
+                const unsigned mask = (unsigned)__shfl((int)lmask, src);
+                const uint32_t b = (uint32_t)__shfl((int)cb, src), e = (uint32_t)__shfl((int)ce, src);
+                kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t, const float (&x)[D], float cl) {
+                    const unsigned long long wcl = kpp_w(cl, s);
 #pragma unroll
-                for (int q = 0; q < KPP_LMAX; ++q) {
-                    if (!((mask >> q) & 1u)) continue;
-                    const float d = dist_canon<D>(x, s_cand[q]);
-                    if (d < cl) dw[q] += wcl - kpp_w(d, s);
-                }
-            });
+                    for (int q = 0; q < KPP_LMAX; ++q) {
+                        if (!((mask >> q) & 1u)) continue;
+                        const float d = dist_canon<D>(x, s_cand[q]);
+                        if (d < cl) dw[q] += wcl - kpp_w(d, s);
+                    }
+                });
+            }
         }
     } else {
         // this wave's items wid, wid + nw, ... (ipw of them): their reach tests
