@@ -52,6 +52,7 @@ struct pcm_engine {
     QExp qe{};
     long long ntiles = 0;            // host copy: -1 = not read back yet (pcm_layout_info reads it)
     long long ntiles_cap = 0;        // upper bound on the tiles of the current layout (grid sizing)
+    uint32_t tile_cap = TILE;        // points per tile
     // device buffers (persistent: grown on demand, reused by later layouts, freed at destroy)
     void *xs = nullptr;
     uint32_t *perm = nullptr;
@@ -410,8 +411,15 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     choose_grid(e);
     const long long nc = e->g.ncells;
     const size_t ts = tsize(e->dtype);
-    // every cell holds ceil(count / TILE) <= count / TILE + 1 tiles
-    e->ntiles_cap = nc + n / TILE + 1;
+    // points per tile (<= TILE): PCM_TILE_CAP for tuning sweeps only
+    static const uint32_t tcap = [] {
+        const char *v = std::getenv("PCM_TILE_CAP");
+        const int c = v ? std::atoi(v) : TILE;
+        return (uint32_t)std::min(TILE, std::max(4 * TPB, c));
+    }();
+    e->tile_cap = tcap;
+    // every cell holds ceil(count / cap) <= count / cap + 1 tiles
+    e->ntiles_cap = nc + n / e->tile_cap + 1;
     e->ntiles = -1;
 
     // persistent layout buffers (no allocation when an earlier layout was as large)
@@ -497,14 +505,14 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     LAUNCHCHK();
     k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, sh, e->cell_start);
     LAUNCHCHK();
-    k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt);
+    k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap);
     LAUNCHCHK();
     size_t sb = scan_bytes;
     if (rocprim::exclusive_scan(tmp, sb, tcnt, e->tile_off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s) != hipSuccess)
         return fail(PCM_E_HIP, "layout: tile scan");
     k_tile_total<<<1, 64, 0, s>>>(e->tile_off, tcnt, nc, e->ntiles_dev);
     LAUNCHCHK();
-    k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles);
+    k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles, e->tile_cap);
     LAUNCHCHK();
     // stream-ordered: no host synchronisation (work queued later on `stream`
     // sees the layout; X must not be modified by other streams meanwhile)

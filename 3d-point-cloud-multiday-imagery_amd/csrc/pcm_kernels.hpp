@@ -306,11 +306,11 @@ __global__ __launch_bounds__(256) void k_cell_starts(const uint32_t *__restrict_
 }
 
 __global__ __launch_bounds__(256) void k_tile_counts(const uint32_t *__restrict__ start, long long ncells,
-                                                     uint32_t *__restrict__ cnt) {
+                                                     uint32_t *__restrict__ cnt, uint32_t cap) {
     long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (c >= ncells) return;
     uint32_t n = start[c + 1] - start[c];
-    cnt[c] = (n + TILE - 1) / TILE;
+    cnt[c] = (n + cap - 1) / cap;
 }
 
 // inv[perm[i]] = i (original row -> sorted position)
@@ -330,13 +330,13 @@ __global__ void k_tile_total(uint32_t *__restrict__ off, const uint32_t *__restr
 }
 
 __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__ start, const uint32_t *__restrict__ off,
-                                                    long long ncells, uint4 *__restrict__ tiles) {
+                                                    long long ncells, uint4 *__restrict__ tiles, uint32_t cap) {
     long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (c >= ncells) return;
     uint32_t s = start[c], e = start[c + 1];
     uint32_t n = e - s;
     if (n == 0) return;
-    uint32_t nt = (n + TILE - 1) / TILE;
+    uint32_t nt = (n + cap - 1) / cap;
     uint32_t per = (n + nt - 1) / nt;
     uint32_t o = off[c];
     for (uint32_t t = 0; t < nt; ++t) {
