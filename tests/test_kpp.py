@@ -138,3 +138,16 @@ def test_gpu_heightmap_like(gpu):
     c_ref, i_ref = P.kmeanspp(X, 96, 21)
     c, i = pcm.kmeans_plusplus(torch.from_numpy(X).cuda(), 96, random_state=21)
     np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,seed", [(5_000_000, 12, 3), (140_000_000, 3, 4)])
+def test_gpu_large_search_segments(gpu, n, k, seed):
+    """k_kpp_search at sizes whose wave segments span several 64-wide chunks of
+    block sums (5M points: 2 chunks per wave) and more chunks than the register
+    cache holds (140M points: 34 > KPP_SCU = 32, the re-read path)."""
+    torch, pcm = gpu
+    X = R.splitmix_uniform(n, 3, seed=seed + 300)
+    _, i_ref = P.kmeanspp(X, k, seed)
+    _, i = pcm.kmeans_plusplus(torch.from_numpy(X).cuda(), k, random_state=seed)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
