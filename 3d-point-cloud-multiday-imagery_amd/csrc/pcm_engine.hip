@@ -703,7 +703,7 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
                         A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
             };
             if (D <= 3 && lloyd_slots(e) == 8) launch(std::integral_constant<int, 8>{});
-            else launch(std::integral_constant<int, LSLOT>{});
+            else launch(std::integral_constant<int, LSLOT>{});   // (8 slots + masks on coarse grids: 42.0 -> 51.2 us at 12.5M)
             LAUNCHCHK();
         }
         return timing_mark(e, 2, s);

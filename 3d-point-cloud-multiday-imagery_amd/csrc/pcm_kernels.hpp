@@ -1363,8 +1363,16 @@ constexpr int LSPEC = 16;   // list records loaded before the count is known
 #define PCM_MASK_MIN 2
 #endif
 constexpr int MASK_MIN = PCM_MASK_MIN;   // sub-cell masks for lists of at least this length
+// Minimum waves per SIMD the compiler must fit (a VGPR budget): the fine-grid
+// fp32 variant (LS = 8, no masks) fits 6 without spilling (70 VGPRs instead of
+// 82 at 4: 10 -> 12 resident blocks per CU; config 3 assign 214.7 -> 209.8 us,
+// tools/wpe_sweep.sh); the masked 16-slot variant spills at 6 (12.5M shard
+// 42.0 -> 45.5 us) and D = 4 gains nothing, so they keep 4.
 template <typename T, int D, int LS, bool MASK>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8))) void k_lloyd1(
+constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? 6 : PCM_WPE; }
+
+template <typename T, int D, int LS, bool MASK>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<T, D, LS, MASK>(), 8))) void k_lloyd1(
     LloydArgs A, const uint4 *__restrict__ tiles, const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
     const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LS+1)*(D+1)][AW]
