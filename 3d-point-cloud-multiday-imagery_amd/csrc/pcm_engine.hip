@@ -702,8 +702,10 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
                     k_lloyd1<TT, D, LS, (D <= 3 && LS == LSLOT)><<<lloyd_grid(e), TPB, lds, s>>>(
                         A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
             };
+            // coarse grids keep 16 slots with masks: 8 slots + LDS int64 words 42.0 -> 51.2 us,
+            // 12 slots + global atomics 42.6 -> 65.7 us at 12.5M (tools/mls_sweep.sh)
             if (D <= 3 && lloyd_slots(e) == 8) launch(std::integral_constant<int, 8>{});
-            else launch(std::integral_constant<int, LSLOT>{});   // (8 slots + masks on coarse grids: 42.0 -> 51.2 us at 12.5M)
+            else launch(std::integral_constant<int, LSLOT>{});
             LAUNCHCHK();
         }
         return timing_mark(e, 2, s);

@@ -1132,7 +1132,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
 #ifdef PCM_OVF_ALL
     constexpr bool kOvf = true;
 #else
-    constexpr bool kOvf = D >= 4 || LS < LSLOT;
+    constexpr bool kOvf = D >= 4 || LS <= 8;   // 8 slots: LDS int64 words past them; 12 / 16: global atomics (rare positions)
 #endif
     __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
     const int tid = threadIdx.x;
@@ -1381,7 +1381,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
 #ifdef PCM_OVF_ALL
     constexpr bool kOvf = true;
 #else
-    constexpr bool kOvf = D >= 4 || LS < LSLOT;
+    constexpr bool kOvf = D >= 4 || LS <= 8;   // 8 slots: LDS int64 words past them; 12 / 16: global atomics (rare positions)
 #endif
     __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
     const int tid = threadIdx.x;
