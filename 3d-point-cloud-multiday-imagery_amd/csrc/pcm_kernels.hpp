@@ -1365,8 +1365,10 @@ constexpr int LSPEC = 16;   // list records loaded before the count is known
 constexpr int MASK_MIN = PCM_MASK_MIN;   // sub-cell masks for lists of at least this length
 // Minimum waves per SIMD the compiler must fit (a VGPR budget): the fine-grid
 // fp32 variant (LS = 8, no masks) fits 6 without spilling (70 VGPRs instead of
-// 82 at 4: 10 -> 12 resident blocks per CU; config 3 assign 214.7 -> 209.8 us,
-// tools/wpe_sweep.sh); the masked 16-slot variant spills at 6 (12.5M shard
+// 82 at 4: 10 -> 12 resident blocks per CU; config 3 assign 214.7 -> 209.8 us
+// on one box, tools/wpe_sweep.sh -- across boxes the rocprof average moved
+// only 212.5 -> 211.3 us: the kernel is memory-bound, residency was not the
+// limit); the masked 16-slot variant spills at 6 (12.5M shard
 // 42.0 -> 45.5 us) and D = 4 gains nothing, so they keep 4.
 template <typename T, int D, int LS, bool MASK>
 constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? 6 : PCM_WPE; }
