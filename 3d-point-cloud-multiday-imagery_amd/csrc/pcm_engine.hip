@@ -555,7 +555,7 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
 
 // Candidate blocks per coarse cell: enough blocks to fill the chip on small
 // (sharded) clouds; D = 4 coarse cells hold 256 fine cells.
-// Measured (tools/r2_sweep.sh): 12.5M-point shard (64 coarse cells) 8 -> 39 us
+// Measured (round-2 bpc sweep, tools/sweep.sh PCM_CAND_BPC_RT): 12.5M-point shard (64 coarse cells) 8 -> 39 us
 // vs 4 -> 47 us per update; 100M (512 coarse cells) 1; D = 4, K = 4096: 32.
 static int cand_bpc(const pcm_engine *e) {
     if (const char *ov = std::getenv("PCM_CAND_BPC_RT")) return std::max(1, std::atoi(ov));   // tuning sweeps only
