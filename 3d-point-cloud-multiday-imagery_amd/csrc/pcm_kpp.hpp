@@ -463,6 +463,13 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
             }
         }
     }
+    // waves that reached no cell hold zeros: skip their L wave reductions (in the
+    // late steps most of the grid's waves have no item, and 8 x 12 cross-lane
+    // moves per idle wave were a large share of the launch)
+    unsigned long long nz = 0ull;
+#pragma unroll
+    for (int q = 0; q < KPP_LMAX; ++q) nz |= dw[q];
+    if (__ballot(nz != 0ull) == 0ull) return;   // wave-uniform
 #pragma unroll
     for (int q = 0; q < KPP_LMAX; ++q) {
         if (q >= L) break;
