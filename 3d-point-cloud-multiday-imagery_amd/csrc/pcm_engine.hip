@@ -1191,15 +1191,21 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
         k_kpp_init<D><<<pgrid, 256, 0, s>>>(xs, perm, cell_start, nc, X, first_index, scale, closest, cmax, bsum, ctl,
                                             (long long *)indices);
         LAUNCHCHK();
+        // from centre 64 on a step touches a neighbourhood: a quarter of the grid
+        // (2048 -> 512 blocks) for eval/apply, 163.3 -> 159.1 ms at config 3
+        // (tools/kpp_grid_sweep.sh; 1/8: 162.6 ms).  PCM_KPP_LATE_*: tuning only
+        static const int late_div = [] { const char *v = std::getenv("PCM_KPP_LATE_DIV"); return v ? std::max(1, std::atoi(v)) : 4; }();
+        static const int late_c = [] { const char *v = std::getenv("PCM_KPP_LATE_C"); return v ? std::atoi(v) : 64; }();
         for (int c = 1; c < k; ++c) {
+            const int eg = c >= late_c ? std::max(ncu, pgrid / late_div) : pgrid;
             k_kpp_search<D><<<L + KPP_RED_BLOCKS, KPP_STPB, 0, s>>>(bsum, nb, closest, inv, X, n,
                                                                     um + (size_t)(c - 1) * L, L, scale, c, cmax, nc,
                                                                     ctl);
             LAUNCHCHK();
-            k_kpp_eval<D><<<pgrid, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
+            k_kpp_eval<D><<<eg, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
             LAUNCHCHK();
-            k_kpp_apply<D><<<pgrid, 256, 0, s>>>(xs, perm, cell_start, g, closest, cmax, bsum, L, scale, c,
-                                                 c + 1 < k ? 1 : 0, (long long *)indices, ctl);
+            k_kpp_apply<D><<<eg, 256, 0, s>>>(xs, perm, cell_start, g, closest, cmax, bsum, L, scale, c,
+                                              c + 1 < k ? 1 : 0, (long long *)indices, ctl);
             LAUNCHCHK();
         }
         return 0;
