@@ -14,7 +14,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 SO_PATH = os.environ.get("PCM_SO") or os.path.join(PKG_DIR, "libpcmkm.so")
-UNITS = [os.path.join(PKG_DIR, "csrc", u) for u in ("pcm_engine.hip", "pcm_dense.hip", "pcm_stereo.hip")]
+UNITS = [os.path.join(PKG_DIR, "csrc", u) for u in ("pcm_engine.hip", "pcm_dense.hip", "pcm_stereo.hip", "pcm_shard.hip")]
 SOURCES = UNITS + [os.path.join(PKG_DIR, "csrc", h) for h in ("pcm_kernels.hpp", "pcm_kpp.hpp", "pcm_cloud.hpp",
                                                               "pcm_common.hpp")] + \
     [os.path.join(REPO_DIR, "include", "pcm_kmeans.h")]
@@ -32,8 +32,10 @@ EXPORTS = [
     "pcm_dense_create", "pcm_dense_destroy", "pcm_dense_begin", "pcm_dense_iterate", "pcm_dense_final",
     "pcm_dense_status", "pcm_dense_outputs", "pcm_dense_kmeanspp_workspace", "pcm_dense_kmeanspp",
     "pcm_photoconsistency", "pcm_lr_consistency",
+    "pcm_layout_shard", "pcm_shard_hist", "pcm_shard_partition_workspace", "pcm_shard_partition",
+    "pcm_shard_scatter_labels", "pcm_assign_kernel_name",
 ]
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lock = threading.Lock()
 _lib = None
@@ -114,6 +116,12 @@ def _declare(lib):
         "pcm_dense_kmeanspp": ([P, I64, I, I, I, I, I64, P, I, P, P, ctypes.c_size_t, P], I),
         "pcm_photoconsistency": ([P, P, I, P, I64, I64, D, P, P], I),
         "pcm_lr_consistency": ([P, P, I64, I64, D, D, P, P, D, P], I),
+        "pcm_layout_shard": ([P, P, I64, P], I),
+        "pcm_shard_hist": ([P, I, I64, I, I, D, D, I, P, P], I),
+        "pcm_shard_partition_workspace": ([I64, I, ctypes.POINTER(ctypes.c_size_t)], I),
+        "pcm_shard_partition": ([P, I, I64, I, I, D, D, I, P, I, I64, P, P, P, P, ctypes.c_size_t, P], I),
+        "pcm_shard_scatter_labels": ([P, P, I64, I64, P, P], I),
+        "pcm_assign_kernel_name": ([P, ctypes.c_char_p, ctypes.c_size_t], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

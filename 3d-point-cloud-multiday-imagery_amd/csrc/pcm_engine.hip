@@ -46,6 +46,10 @@ int pcm_fail(int code, const std::string &msg) { return fail(code, msg); }
 struct pcm_engine {
     int device = 0, d = 3, k = 1, dtype = PCM_F32, max_iter_cap = 300;
     long long n = 0, npad = 0, gidx0 = 0;
+    long long n_global = 0;          // points over all ranks (pcm_layout_shard; = n for a single-process fit)
+    uint32_t *grows = nullptr;       // global row of every local point (spatial shard) or null: gidx0 + i
+    size_t cap_grows = 0;
+    bool has_rows = false;
     double lo[MAXD] = {0}, hi[MAXD] = {0}, maxabs[MAXD] = {0};
     bool have_bbox = false, layout_ready = false, fit_ready = false;
     Grid g{};
@@ -247,7 +251,9 @@ void make_grid(Grid &g, int d, const double *lo, const double *hi, double target
 void choose_grid(pcm_engine *e) {
     // D = 4: smaller cells (~1k points) shorten the lists more than the tiles
     // cost (config-5 shape: 20736 -> 65536 cells, 913 -> 846 us per iteration)
-    double target = std::min(32.0 * e->k, (double)e->n / (e->d >= 4 ? 1000.0 : 2800.0));
+    // (a spatial shard holds about n / n_global of the centres: the cap scales with it)
+    const double share = e->n_global > 0 ? std::min(1.0, (double)e->n / (double)e->n_global) : 1.0;
+    double target = std::min(32.0 * e->k * share, (double)e->n / (e->d >= 4 ? 1000.0 : 2800.0));
     if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     make_grid(e->g, e->d, e->lo, e->hi, target);
     if (e->k <= 1) e->g.prune = 0;
@@ -345,7 +351,8 @@ int pcm_engine_destroy(pcm_engine *e) {
             if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
     free_buffers(e);
     void *ps[] = {e->C, e->Cn, e->cref, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
-                  e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx, e->ntiles_dev};
+                  e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx, e->ntiles_dev,
+                  e->grows};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -358,6 +365,8 @@ int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream, doubl
     if (int rc = check_device(e)) return rc;
     hipStream_t s = (hipStream_t)stream;
     e->n = n;
+    e->n_global = n;
+    e->has_rows = false;
     e->have_bbox = false;
     free_layout(e);
     if (n == 0) {
@@ -393,6 +402,21 @@ int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream, doubl
 }
 
 static int lloyd_slots(const pcm_engine *e);
+
+int pcm_layout_shard(pcm_engine *e, const uint32_t *rows, int64_t n_global, void *stream) {
+    if (!e || (!rows && e->n > 0)) return fail(PCM_E_ARG, "bad argument");
+    if (!e->have_bbox) return fail(PCM_E_STATE, "pcm_layout_bbox must run first");
+    if (n_global < e->n || n_global >= (1LL << 32)) return fail(PCM_E_ARG, "n_global must be in [n, 2^32)");
+    if (int rc = check_device(e)) return rc;
+    free_layout(e);
+    e->n_global = n_global;
+    e->has_rows = true;
+    if (e->n == 0) return 0;
+    HIPCHK(ensure(e->grows, e->cap_grows, (size_t)e->n * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(e->grows, rows, (size_t)e->n * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                          (hipStream_t)stream));
+    return 0;
+}
 
 int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gidx0, void *stream) {
     if (!e || !q) return fail(PCM_E_ARG, "bad argument");
@@ -595,7 +619,9 @@ static int lloyd_grid(const pcm_engine *e) { return (int)std::max(1LL, e->ntiles
 
 static int lloyd_slots(const pcm_engine *e) {
     if (const char *ov = std::getenv("PCM_LSLOT_RT")) return std::atoi(ov) == 8 ? 8 : LSLOT;   // tuning sweeps only
-    return (e->g.prune && e->g.ncells >= 8LL * e->k) ? 8 : LSLOT;
+    // cells per centre of the whole cloud (a spatial shard's cells cover ~n / n_global of the centres)
+    const double share = e->n_global > 0 ? std::min(1.0, (double)e->n / (double)e->n_global) : 1.0;
+    return (e->g.prune && (double)e->g.ncells >= 8.0 * e->k * share) ? 8 : LSLOT;
 }
 
 static LloydArgs lloyd_args(pcm_engine *e) {
@@ -834,7 +860,8 @@ int pcm_reloc_candidates(pcm_engine *e, int m, void *records, void *stream) {
         return dispatch_l(e, [&](auto L) -> int {
             using LT = decltype(L);
             k_reloc_keys<TT, D, LT><<<blocks_for(n), 256, 0, s>>>((const TT *)e->xs, n, (const LT *)e->lab, e->perm,
-                                                                 e->C, e->gidx0, keys);
+                                                                 e->C, e->gidx0, e->has_rows ? e->grows : nullptr,
+                                                                 keys);
             LAUNCHCHK();
             if (m < n)   // exactly the top m; m >= n takes every point (T = 0)
                 for (int pass = 0; pass < 8; ++pass) {
@@ -980,6 +1007,16 @@ int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid) 
     }
     *ntiles = e->ntiles;
     for (int a = 0; a < MAXD; ++a) grid[a] = e->g.G[a];
+    return 0;
+}
+
+int pcm_assign_kernel_name(pcm_engine *e, char *buf, size_t n) {
+    if (!e || !buf || n == 0) return fail(PCM_E_ARG, "bad argument");
+    if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
+    const int ls = (e->d <= 3 && lloyd_slots(e) == 8) ? 8 : LSLOT;
+    const bool mask = e->d <= 3 && ls == LSLOT;
+    std::snprintf(buf, n, "k_lloyd1<%s,%d,%d,%s>", e->dtype == PCM_F16 ? "__half" : "float", e->d, ls,
+                  mask ? "true" : "false");
     return 0;
 }
 

@@ -2070,13 +2070,15 @@ template <typename T, int D, typename LT>
 __global__ __launch_bounds__(256) void k_reloc_keys(const T *__restrict__ xs, long long n,
                                                     const LT *__restrict__ lab, const uint32_t *__restrict__ perm,
                                                     const float4 *__restrict__ C, long long gidx0,
+                                                    const uint32_t *__restrict__ grows,
                                                     unsigned long long *__restrict__ keys) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= n) return;
     float x[D];
     for (int a = 0; a < D; ++a) x[a] = to_f<T>(xs[xs_index<D>(i, a)]);
     float d = dist_canon<D>(x, C[(int)lab[i]]);
-    unsigned long long g = (unsigned long long)(gidx0 + perm[i]);
+    const uint32_t r = perm[i];
+    unsigned long long g = grows ? (unsigned long long)grows[r] : (unsigned long long)(gidx0 + r);
     keys[i] = ((unsigned long long)__float_as_uint(d) << 32) | (0xffffffffull - (g & 0xffffffffull));
 }
 

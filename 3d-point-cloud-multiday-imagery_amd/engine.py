@@ -87,6 +87,25 @@ class Engine:
         self.stats = torch.zeros(cnt.value, dtype=torch.int64, device=self.device)
         _lib.check(self.lib.pcm_bind_stats(self.h, _ptr(self.stats)), "pcm_bind_stats")
 
+    def set_shard(self, rows: torch.Tensor, n_global: int):
+        """This engine's cloud is a spatial shard (``pcm_layout_shard``): global
+        row of every local point (relocation tie-break), points on all ranks."""
+        rows = rows.to(device=self.device, dtype=torch.int32).contiguous()
+        if rows.numel() != self.n:
+            raise ValueError("one global row per local point")
+        _lib.check(self.lib.pcm_layout_shard(self.h, _ptr(rows) if rows.numel() else None, int(n_global), _stream()),
+                   "pcm_layout_shard")
+
+    # spatial slab sharding (stateless operators, csrc/pcm_shard.hip)
+    def shard_hist(self, X, axis, lo, inv, nbins):
+        return shard_hist(X, axis, lo, inv, nbins)
+
+    def shard_partition(self, X, axis, lo, inv, nbins, owner, world, gidx0):
+        return shard_partition(X, axis, lo, inv, nbins, owner, world, gidx0)
+
+    def shard_scatter_labels(self, labels, rows, gidx0, n):
+        return shard_scatter_labels(labels, rows, gidx0, n)
+
     def _check_points(self, X: torch.Tensor) -> torch.Tensor:
         if X.dim() != 2 or X.shape[1] != self.d:
             raise ValueError(f"points must be (N, {self.d})")
@@ -167,11 +186,63 @@ class Engine:
         _lib.check(self.lib.pcm_layout_info(self.h, ctypes.byref(nc), ctypes.byref(nt), g), "pcm_layout_info")
         return dict(ncells=nc.value, ntiles=nt.value, grid=list(g)[: self.d])
 
+    def assign_kernel(self) -> str:
+        buf = ctypes.create_string_buffer(128)
+        _lib.check(self.lib.pcm_assign_kernel_name(self.h, buf, 128), "pcm_assign_kernel_name")
+        return buf.value.decode()
+
     def candidate_stats(self) -> dict:
         mean, mx, full = ctypes.c_double(), ctypes.c_int(), ctypes.c_int64()
         _lib.check(self.lib.pcm_candidate_stats(self.h, ctypes.byref(mean), ctypes.byref(mx), ctypes.byref(full),
                                                 _stream()), "pcm_candidate_stats")
         return dict(mean=mean.value, max=mx.value, full_cells=full.value)
+
+
+def _dtype_code(X: torch.Tensor) -> int:
+    if X.dtype == torch.float32:
+        return PCM_F32
+    if X.dtype == torch.float16:
+        return PCM_F16
+    raise ValueError("points dtype must be float32 or float16")
+
+
+def shard_hist(X: torch.Tensor, axis: int, lo: float, inv: float, nbins: int) -> torch.Tensor:
+    """Histogram (int64, device) of bin = clamp(floor((X[:, axis] - lo) * inv)) (``pcm_shard_hist``)."""
+    lib = _lib.load()
+    X = X.contiguous()
+    hist = torch.empty(nbins, dtype=torch.int64, device=X.device)
+    _lib.check(lib.pcm_shard_hist(_ptr(X) if X.numel() else None, _dtype_code(X), X.shape[0], X.shape[1], int(axis),
+                                  float(lo), float(inv), int(nbins), _ptr(hist), _stream()), "pcm_shard_hist")
+    return hist
+
+
+def shard_partition(X: torch.Tensor, axis: int, lo: float, inv: float, nbins: int, owner, world: int, gidx0: int):
+    """Stable partition of the rows by ``owner[bin]`` (``pcm_shard_partition``):
+    (rows grouped by destination, their global indices as int32, counts)."""
+    lib = _lib.load()
+    X = X.contiguous()
+    n, d = X.shape
+    own = torch.as_tensor(np.ascontiguousarray(owner, dtype=np.uint8), device=X.device)
+    out = torch.empty_like(X)
+    rows = torch.empty(n, dtype=torch.int32, device=X.device)
+    counts = np.zeros(world, dtype=np.int64)
+    ws_bytes = ctypes.c_size_t()
+    _lib.check(lib.pcm_shard_partition_workspace(n, int(world), ctypes.byref(ws_bytes)), "pcm_shard_partition_workspace")
+    ws = torch.empty(max(1, ws_bytes.value), dtype=torch.uint8, device=X.device)
+    _lib.check(lib.pcm_shard_partition(_ptr(X) if n else None, _dtype_code(X), n, d, int(axis), float(lo), float(inv),
+                                       int(nbins), _ptr(own), int(world), int(gidx0), _ptr(out) if n else None,
+                                       _ptr(rows) if n else None, counts.ctypes.data_as(ctypes.c_void_p), _ptr(ws),
+                                       ws_bytes.value, _stream()), "pcm_shard_partition")
+    return out, rows, counts
+
+
+def shard_scatter_labels(labels: torch.Tensor, rows: torch.Tensor, gidx0: int, n: int) -> torch.Tensor:
+    """out[rows[i] - gidx0] = labels[i] (``pcm_shard_scatter_labels``)."""
+    lib = _lib.load()
+    out = torch.empty(n, dtype=torch.int32, device=labels.device)
+    _lib.check(lib.pcm_shard_scatter_labels(_ptr(labels) if n else None, _ptr(rows) if n else None, int(n), int(gidx0),
+                                            _ptr(out) if n else None, _stream()), "pcm_shard_scatter_labels")
+    return out
 
 
 def synth_uniform(n: int, d: int, seed: int, start: int = 0, device=None) -> torch.Tensor:

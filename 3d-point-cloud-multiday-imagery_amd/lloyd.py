@@ -14,13 +14,16 @@ Restates the control flow of scikit-learn's ``_kmeans_single_lloyd``
   host gathers every rank's farthest points and resumes;
 * the final E-step + inertia (``_kmeans.py:736-750``) is ``Engine.final``.
 
-Multi-GPU: rank r owns a contiguous row shard; the only collective on the data
-path is one SUM all-reduce of K*(D+1)+1 int64 per iteration (RCCL over xGMI with
-the ``nccl`` backend).  Integer statistics make the result bit-identical for
-any world size.
+Multi-GPU: rank r receives a contiguous row shard; at layout time the shards are
+regrouped into equal-count spatial slabs (one all_to_all of the points; the
+labels travel back after the final E-step).  The only collective per iteration
+is one SUM all-reduce of K*(D+1)+1 int64 (RCCL over xGMI with the ``nccl``
+backend).  Integer statistics make the result bit-identical for any world size
+and any sharding.
 """
 from __future__ import annotations
 
+import warnings
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -62,40 +65,111 @@ def _world(group):
     return 1, 0
 
 
-def prepare(engine, X, group=None):
-    """Layout phase: global fixed-point exponents, shard offsets, cell sort."""
+SLAB_BINS = 16384   # slab histogram resolution (pcm_shard_hist's LDS bound)
+
+
+def slab_owner(hist: np.ndarray, world: int) -> np.ndarray:
+    """Bin -> rank of the equal-count slab cut: bin b goes to the rank whose
+    share [r N / P, (r + 1) N / P) holds the bin's midpoint count.  Monotone in
+    b, so every rank owns one contiguous slab of the axis."""
+    h = np.asarray(hist, dtype=np.int64)
+    total = int(h.sum())
+    if total == 0:
+        return np.zeros(h.shape[0], np.uint8)
+    before = np.cumsum(h) - h
+    return np.minimum(world - 1, ((2 * before + h) * world) // (2 * total)).astype(np.uint8)
+
+
+def prepare(engine, X, group=None, shard: str = "auto"):
+    """Layout phase: global fixed-point exponents, shard offsets, cell sort.
+
+    ``shard`` (world > 1): "slab" (= "auto") regroups the ranks' row shards into
+    equal-count slabs of the longest axis of the global bounding box (one
+    all_to_all of the points at layout time; labels travel back in ``finish``),
+    so each rank's pruning grid covers only its slab and its per-iteration work
+    shrinks with the world size; "rows" keeps the row shards in place."""
     import torch.distributed as dist
     world, rank = _world(group)
-    _, _, maxabs = engine.bbox(X)
     n_local = int(X.shape[0])
-    gidx0, n_total = 0, n_local
-    if world > 1:
-        dev = engine.stats_device
-        m = torch.tensor(np.asarray(maxabs, dtype=np.float64), device=dev)
-        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
-        maxabs = m.cpu().numpy()
-        mine = torch.tensor([n_local], dtype=torch.int64, device=dev)
-        parts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(parts, mine, group=group)
-        counts = [int(p.item()) for p in parts]
-        gidx0, n_total = sum(counts[:rank]), sum(counts)
+    lo, hi, maxabs = engine.bbox(X)
+    engine._slab = None
+    if world == 1:
+        q = fixed_q(maxabs)
+        engine.build(X, q, 0)
+        return q, n_local
+    if shard not in ("auto", "slab", "rows"):
+        raise ValueError("shard must be 'auto', 'slab' or 'rows'")
+    dev = engine.stats_device
+    mine = torch.tensor([n_local], dtype=torch.int64, device=dev)
+    parts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    counts = [int(p.item()) for p in parts]
+    gidx0, n_total = sum(counts[:rank]), sum(counts)
     if n_total >= 2 ** 32:
         raise ValueError("at most 2**32 - 1 points in one fit")
+    lo = np.asarray(lo, np.float64) if n_local else np.full(engine.d, np.inf)
+    hi = np.asarray(hi, np.float64) if n_local else np.full(engine.d, -np.inf)
+    m = torch.tensor(np.concatenate([-lo, hi, np.asarray(maxabs, np.float64)]), device=dev)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+    m = m.cpu().numpy()
+    d = engine.d
+    glo, ghi, maxabs = -m[:d], m[d:2 * d], m[2 * d:]
     q = fixed_q(maxabs)
-    engine.build(X, q, gidx0)
+    if shard == "rows" or n_total == 0:
+        engine.build(X, q, gidx0)
+        return q, n_total
+    ext = ghi - glo
+    axis = int(np.argmax(ext))
+    inv = SLAB_BINS / ext[axis] if ext[axis] > 0 else 0.0
+    hist = engine.shard_hist(X, axis, glo[axis], inv, SLAB_BINS)
+    dist.all_reduce(hist, group=group)
+    owner = slab_owner(hist.cpu().numpy(), world)
+    Xs, rows, send = engine.shard_partition(X, axis, glo[axis], inv, SLAB_BINS, owner, world, gidx0)
+    st = torch.tensor(send, dtype=torch.int64, device=dev)
+    rt = torch.empty_like(st)
+    dist.all_to_all_single(rt, st, group=group)
+    recv = rt.cpu().numpy().astype(np.int64)
+    sl, rl = [int(v) for v in send], [int(v) for v in recv]
+    Xr = torch.empty((sum(rl), d), dtype=X.dtype, device=X.device)
+    dist.all_to_all_single(Xr, Xs, rl, sl, group=group)
+    rows_r = torch.empty(sum(rl), dtype=torch.int32, device=X.device)
+    dist.all_to_all_single(rows_r, rows, rl, sl, group=group)
+    del Xs
+    engine.bbox(Xr)
+    engine.set_shard(rows_r, n_total)
+    engine.build(Xr, q, 0)
+    engine._slab = dict(rows=rows, send=sl, recv=rl, gidx0=gidx0, n_local=n_local, axis=axis,
+                        n_slab=sum(rl))
     return q, n_total
 
 
 def _uses_graph(graph, world, group, split):
+    """HIP-graph replay of the multi-GPU iteration sequence: opt-in (``graph=True``
+    or ``PCM_LLOYD_GRAPH=1``) and only with RCCL, whose collectives can be
+    captured (gloo's cannot)."""
+    import os
+
     import torch.distributed as dist
-    if graph is not None:
-        return bool(graph)
-    if not (world > 1 or split) or not dist.is_initialized():
+    if graph is None:
+        graph = os.environ.get("PCM_LLOYD_GRAPH", "0") == "1"
+    if not graph or not (world > 1 or split) or not dist.is_initialized():
         return False
     try:
-        return dist.get_backend(group) == "nccl"   # RCCL collectives can be captured; gloo's cannot
+        return dist.get_backend(group) == "nccl"
     except Exception:   # noqa: BLE001
         return False
+
+
+def agree(ok: bool, world: int, group=None, device=None) -> bool:
+    """True only if ``ok`` holds on every rank (MIN all-reduce of a flag), so that
+    all ranks take the same path (captured graph vs eager launches) and their
+    collective sequences stay aligned."""
+    if world <= 1:
+        return ok
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
 
 
 def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, graph=None):
@@ -104,8 +178,8 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, gra
     One process: ``pcm_iterate`` (k_lloyd + fused k_step per iteration).  Several
     (or ``split``): ``iter_local`` (k_lloyd accumulating into the statistics
     buffer) -> all-reduce of the statistics (only when world > 1) ->
-    ``iter_global`` (k_step on them).  With RCCL (``graph`` None = auto) a chunk
-    of that sequence is captured once in a HIP graph and replayed: no host launch
+    ``iter_global`` (k_step on them).  With RCCL and ``graph`` (opt-in, see
+    ``_uses_graph``) a chunk of that sequence is captured once in a HIP graph and replayed: no host launch
     gaps between the kernels and the collective; the device control block gates
     iterations queued past convergence or a halt either way."""
     import torch
@@ -130,13 +204,18 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, gra
             engine.iterate(n_enq)
         elif use_graph and n_enq == chunk:
             if captured is None:
+                ok = True
                 try:
                     captured = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(captured):
                         seq(chunk)
-                except Exception:   # noqa: BLE001 -- capture refused: eager launches
-                    captured, use_graph = None, False
+                except Exception as exc:   # noqa: BLE001 -- capture refused: eager launches
+                    ok = False
+                    warnings.warn(f"pcm_amd.lloyd: HIP-graph capture failed ({exc!r}); eager launches")
                     torch.cuda.synchronize()
+                # every rank takes the same path (capture records the collectives without running them)
+                if not agree(ok, world, group, engine.stats_device):
+                    captured, use_graph = None, False
                     seq(n_enq)
             if captured is not None:
                 captured.replay()
@@ -161,6 +240,14 @@ def finish(engine, group=None):
     import torch.distributed as dist
     world, _ = _world(group)
     engine.final()
+    labels = engine.labels()
+    sl = getattr(engine, "_slab", None)
+    if sl is not None:
+        # the slab's labels travel back to the ranks that own the rows (reverse all_to_all),
+        # then into the caller's row order
+        back = torch.empty(sl["n_local"], dtype=torch.int32, device=labels.device)
+        dist.all_to_all_single(back, labels, sl["send"], sl["recv"], group=group)
+        labels = engine.shard_scatter_labels(back, sl["rows"], sl["gidx0"], sl["n_local"])
     st = engine.status()
     inertia = st["inertia"]
     if world > 1:   # exact integer limbs: the same inertia for any world size
@@ -169,11 +256,11 @@ def finish(engine, group=None):
         dist.all_reduce(t, group=group)
         v = [int(x) for x in t.cpu().tolist()]
         inertia = inertia_from_limbs(v[:3], st["inertia_scale"], v[3])
-    return engine.labels(), engine.centers(), inertia
+    return labels, engine.centers(), inertia
 
 
 def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=None, chunk: int = 8,
-              engine=None, split: bool = False, graph=None) -> LloydResult:
+              engine=None, split: bool = False, graph=None, shard: str = "auto") -> LloydResult:
     """Fit K-means (Lloyd) to this rank's shard ``X`` (N_local, D) from ``centers_init`` (K, D).
 
     ``tol`` is the absolute centre-shift tolerance (sklearn's ``_tolerance``
@@ -185,10 +272,15 @@ def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=N
     if engine is None:
         from .engine import Engine
         engine = Engine(X.shape[1], centers_init.shape[0], X.dtype, max_iter=max_iter)
-    prepare(engine, X, group)
+    prepare(engine, X, group, shard)
     st, relocs = run(engine, centers_init, max_iter, tol, group, chunk, split, graph)
     labels, centers, inertia = finish(engine, group)
     ch, sh = engine.history(int(st["iter"]))
+    layout = engine.layout_info()
+    sl = getattr(engine, "_slab", None)
+    layout["shard"] = "slab" if sl is not None else "rows"
+    if sl is not None:
+        layout["slab_points"] = sl["n_slab"]
+        layout["slab_axis"] = sl["axis"]
     return LloydResult(labels=labels, centers=centers, inertia=inertia, n_iter=int(st["iter"]),
-                       strict=st["done"] == 1, changed=ch, shift=sh, relocations=relocs,
-                       layout=engine.layout_info())
+                       strict=st["done"] == 1, changed=ch, shift=sh, relocations=relocs, layout=layout)

@@ -11,6 +11,15 @@ float64 NumPy cloud assembly of ``plugin.py:147-192`` and the per-pair layers of
   ``disparity_map``; imported lazily, only inside the reference tree) and yields
   one ``PairProducts`` per pair -- the debug image layers it emits before the
   assembly, the disparity, its validity mask and the photoconsistency map;
+* while ``disparity_map`` runs, its L/R-consistency and photoconsistency
+  gathers (``disparity.py:157-161``, the names bound at ``disparity.py:7-9`` and
+  defined at ``disparity.py:229-250`` / ``processing.py:94-115``) resolve to the
+  HIP drop-ins of ``stereo.py`` (``use_gpu_gathers``, row f3);
+* failures keep the reference's error layers: a missing image and a failed crop
+  raise ``ImageNotFound`` / ``CropFailed``, which the plugin turns into
+  ``(np.zeros((100, 100)), {"name": "error: ..."}, "image")``
+  (``plugin.py:77-79, 89-91``); the run log goes to ``TEMP/log.txt``
+  (``plugin.py:49-50, 234, 240``);
 * ``pair_layers(...)`` rebuilds the per-pair layers of ``plugin.py:176-233``
   from the GPU assembly (``cloud.assemble_cloud_device``) -- the height-map
   image (``normalise_for_display`` of the relative heights equals the
@@ -20,7 +29,9 @@ float64 NumPy cloud assembly of ``plugin.py:147-192`` and the per-pair layers of
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import threading
 from dataclasses import dataclass, field
 from typing import Iterator, List
 
@@ -29,6 +40,50 @@ import numpy as np
 PREFIX = "[Multi-day 3D Point Cloud]"
 MASK_COLORMAP = {"colors": [[0.0, 0.0, 0.0, 0.0], [0.0, 0.0, 0.0, 1.0]], "name": "mask_blackout",
                  "interpolation": "linear"}
+
+
+class ImageNotFound(FileNotFoundError):
+    """A stereo image of a selected pair is missing (plugin.py:77-79)."""
+
+
+class CropFailed(RuntimeError):
+    """Cropping an image to the KML region failed (plugin.py:83-91); str() is the cause's message."""
+
+
+GATHER_NAMES = ("left_right_consistency", "photoconsistency_map")
+_gather_lock = threading.Lock()
+_gather_users = 0
+_gather_saved: dict = {}
+
+
+@contextlib.contextmanager
+def use_gpu_gathers(module):
+    """Rebind ``module.left_right_consistency`` / ``module.photoconsistency_map``
+    (the globals ``disparity_map`` resolves at ``disparity.py:157-161``) to the HIP
+    drop-ins for the duration of the block; restored on exit (also on error).
+    Reference-counted, so concurrent plugin runs share one binding."""
+    global _gather_users
+    from . import stereo
+    with _gather_lock:
+        if _gather_users == 0:
+            _gather_saved.clear()
+            for name in GATHER_NAMES:
+                if hasattr(module, name):
+                    _gather_saved[(id(module), name)] = getattr(module, name)
+                setattr(module, name, getattr(stereo, name))
+        _gather_users += 1
+    try:
+        yield module
+    finally:
+        with _gather_lock:
+            _gather_users -= 1
+            if _gather_users == 0:
+                for name in GATHER_NAMES:
+                    key = (id(module), name)
+                    if key in _gather_saved:
+                        setattr(module, name, _gather_saved.pop(key))
+                    else:
+                        delattr(module, name)
 
 
 @dataclass
@@ -68,14 +123,31 @@ def pair_layers(pp: PairProducts, points: np.ndarray, h_norm: np.ndarray) -> lis
 
 
 class ReferenceStereoStages:
-    """plugin.py:45-145 with the reference's functions (runs inside the reference tree)."""
+    """plugin.py:45-145 with the reference's functions (runs inside the reference tree).
+
+    ``gpu_gathers``: run ``disparity_map``'s consistency gathers on the GPU
+    (``use_gpu_gathers``); False keeps the reference's NumPy ones."""
+
+    def __init__(self, gpu_gathers: bool = True):
+        self.gpu_gathers = gpu_gathers
+        self._log = None
+
+    # plugin.py:49-50: the run log, TEMP/log.txt, opened once TEMP exists
+    def log(self, msg: str):
+        if self._log is not None:
+            self._log.write(msg)
+
+    def close_log(self):
+        if self._log is not None:
+            self._log.close()
+            self._log = None
 
     def pairs(self, kml_path, is_debug_mode: bool = True, is_debug_pair: bool = False,
               is_one_random_pair: bool = True, n: int = 10) -> Iterator[PairProducts]:
         import shutil
 
         from members.rafael.disparity import constants as C  # type: ignore
-        from members.rafael.disparity.disparity import disparity_map  # type: ignore
+        from members.rafael.disparity import disparity as dmod  # type: ignore
         from members.rafael.disparity.pair_selector import PairSelector  # type: ignore
         from members.rafael.disparity.preprocessing import generate_cropped, get_crop_area_from_kml  # type: ignore
         from members.rafael.disparity.processing import generate_rectified  # type: ignore
@@ -84,11 +156,16 @@ class ReferenceStereoStages:
         if os.path.exists(C.TEMP_PATH):
             shutil.rmtree(C.TEMP_PATH)
         os.makedirs(C.TEMP_PATH, exist_ok=False)
+        self.close_log()
+        self._log = open(os.path.join(C.TEMP_PATH, "log.txt"), "w")
+        self.log("3D Point Cloud started")
+        self.log(f"loading images from: {C.WV3_PATH}\n")
         selector = PairSelector(C.WV3_PATH)
         selector.discover_images()
         pairs = selector.select_pairs()
         for p in (C.TMP_STEREO_OUTPUT_PATH, C.TMP_CROPPED_IMAGES_PATH, C.TMP_DISPARITY_DEBUG_PATH):
             os.makedirs(p, exist_ok=False)
+        self.log("preprocessing pairs")
         if is_debug_pair:
             a, b = C.PAIR_DECENT_RESULTS[0]
             pairs = [p for p in pairs if {p.img1.filename, p.img2.filename} == {a, b}]
@@ -100,13 +177,28 @@ class ReferenceStereoStages:
             for img in (pair.img1, pair.img2):
                 name = img.filename + ".tif"
                 if not os.path.exists(img.path):
-                    raise FileNotFoundError(f"image not found {img.path}")
-                if not os.path.exists(os.path.join(C.TMP_CROPPED_IMAGES_PATH, name)):
-                    generate_cropped(img, C.TMP_CROPPED_IMAGES_PATH, name, get_crop_area_from_kml(img, str(kml_path)))
+                    self.log(f"image not found  {img.path}")
+                    raise ImageNotFound(img.path)
+                if os.path.exists(os.path.join(C.TMP_CROPPED_IMAGES_PATH, name)):
+                    continue
+                try:
+                    area = get_crop_area_from_kml(img, str(kml_path))
+                    self.log(f"crop area for {img.filename}: {area}")
+                    generate_cropped(img, C.TMP_CROPPED_IMAGES_PATH, name, area)
+                    self.log(f"generated cropped image for {img.filename} at {C.TMP_CROPPED_IMAGES_PATH}")
+                except Exception as e:   # noqa: BLE001 -- plugin.py:89-91
+                    self.log(f"error: Cropping failed for {img.filename}: {str(e)}")
+                    raise CropFailed(str(e)) from e
         for pair_id, pair in enumerate(pairs):
-            generate_rectified(pair, pair_id, C.TMP_STEREO_OUTPUT_PATH)
-            disparity, validity, photo = disparity_map(pair, pair_id, C.TMP_STEREO_OUTPUT_PATH,
-                                                       C.TMP_CROPPED_IMAGES_PATH, C.TMP_DISPARITY_DEBUG_PATH)
+            self.log("ASP stereo rectification...")
+            out_path = generate_rectified(pair, pair_id, C.TMP_STEREO_OUTPUT_PATH)
+            self.log(f"Rectification complete, output: {out_path}")
+            self.log("Generating disparity map...")
+            gathers = use_gpu_gathers(dmod) if self.gpu_gathers else contextlib.nullcontext()
+            with gathers:
+                disparity, validity, photo = dmod.disparity_map(pair, pair_id, C.TMP_STEREO_OUTPUT_PATH,
+                                                                C.TMP_CROPPED_IMAGES_PATH, C.TMP_DISPARITY_DEBUG_PATH)
+            self.log("Disparity map generated successfully")
             image_layers = []
             if is_debug_mode:   # plugin.py:119-145
                 sources = [(os.path.join(C.TMP_CROPPED_IMAGES_PATH, pair.img1.cropped_name), "Input Left"),

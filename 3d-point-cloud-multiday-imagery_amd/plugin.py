@@ -12,8 +12,12 @@ keeps that component's public contract:
 * ``run(kml_path, is_debug_mode=True, is_debug_pair=False,
   is_one_random_pair=True, n=10)`` (plugin.py:36-40, defaults from
   constants.py:5-10), called on a napari worker thread (widget.py:144-147);
-* returns host numpy layers only, and never raises: failures come back as an
-  error image layer (plugin.py:77-79, 89-91, 236-241).
+* returns host numpy layers only, and never raises: failures come back as the
+  reference's error image layers -- ``np.zeros((100, 100))`` named
+  ``"error: image not found"`` / ``"error: <msg>"`` for a missing image or a
+  failed crop (plugin.py:77-79, 89-91), otherwise ``np.ones((100, 100))`` named
+  ``"Error: <msg>"`` (plugin.py:236-241); the stages write the run log
+  ``TEMP/log.txt`` (plugin.py:49-50, 234, 240).
 
 ``run`` replays the reference's per-pair stereo stages (``pipeline.py``:
 pair selection, crop, ASP rectification, SGBM/WLS disparity -- the reference's
@@ -178,9 +182,8 @@ class HeightMapExtractor(SatellitePlugin):
     def name(self):
         return "Multi-day 3D Point Cloud"
 
-    def _gpu_stages_run(self, kml_path, is_debug_mode, is_debug_pair, is_one_random_pair, n) -> List:
-        from .pipeline import ReferenceStereoStages, pair_layers
-        stages = self._stages or ReferenceStereoStages()
+    def _gpu_stages_run(self, stages, kml_path, is_debug_mode, is_debug_pair, is_one_random_pair, n) -> List:
+        from .pipeline import pair_layers
         layers, host_clouds, dev_clouds = [], [], []
         for pp in stages.pairs(kml_path, is_debug_mode=is_debug_mode, is_debug_pair=is_debug_pair,
                                is_one_random_pair=is_one_random_pair, n=n):
@@ -205,12 +208,32 @@ class HeightMapExtractor(SatellitePlugin):
                                               export_path=self.export_path)
         return layers + fused
 
+    def _stages_run(self, kml_path, is_debug_mode, is_debug_pair, is_one_random_pair, n) -> List:
+        from .pipeline import CropFailed, ImageNotFound, ReferenceStereoStages
+        stages = self._stages or ReferenceStereoStages()
+        log = getattr(stages, "log", lambda msg: None)
+        try:
+            layers = self._gpu_stages_run(stages, kml_path, is_debug_mode, is_debug_pair, is_one_random_pair, n)
+            log(f"Added {len(layers)} layers to Napari")
+            return layers
+        except ImageNotFound:                      # plugin.py:77-79
+            return [(np.zeros((100, 100)), {"name": "error: image not found"}, "image")]
+        except CropFailed as e:                    # plugin.py:89-91
+            return [(np.zeros((100, 100)), {"name": f"error: {str(e)}"}, "image")]
+        except Exception as e:                     # plugin.py:236-241
+            import traceback
+            traceback.print_exc()
+            log(f"Error: {str(e)}\n{traceback.format_exc()}")
+            return [(np.ones((100, 100)), {"name": f"Error: {str(e)}"}, "image")]
+        finally:
+            getattr(stages, "close_log", lambda: None)()
+
     def run(self, kml_path, is_debug_mode: bool = DEFAULTS["is_debug_mode"],
             is_debug_pair: bool = DEFAULTS["is_debug_pair"],
             is_one_random_pair: bool = DEFAULTS["is_one_random_pair"], n: int = DEFAULTS["n"]) -> List:
         try:
             if self._base is None:
-                return self._gpu_stages_run(kml_path, is_debug_mode, is_debug_pair, is_one_random_pair, n)
+                return self._stages_run(kml_path, is_debug_mode, is_debug_pair, is_one_random_pair, n)
             layers = list(self._base.run(kml_path, is_debug_mode=is_debug_mode, is_debug_pair=is_debug_pair,
                                          is_one_random_pair=is_one_random_pair, n=n))
             clouds = [data for data, params, kind in layers

@@ -14,11 +14,18 @@ order before the timed region; that one-time layout is reported separately
 as ``layout_ms`` (it is not repeated per iteration).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n N] [--k K] [--d D]
-       (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+  N > 1: either under torchrun (RANK/WORLD_SIZE set by the launcher), or plain
+  ``python bench.py --gpus N``: the parent then starts N rank processes itself
+  (before anything touches the GPU), one per GPU, and exits with their status.
+  Each rank generates its contiguous row shard of the cloud on its GPU; the
+  layout regroups the shards into spatial slabs (one all_to_all, in
+  ``layout_ms``); every timed iteration all-reduces the K*(D+1)+1 statistics.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -137,6 +144,133 @@ def pmc_traffic(n, k, d, world):
     return rd + wr, os.path.relpath(path, ROOT)
 
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script
+    (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment) and wait.  The
+    parent never initialises the GPU.  Any rank failing terminates the others
+    (by their own PIDs) and the parent returns the first failure's status."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def slab_proxy(args) -> dict:
+    """Config 4 at P GPUs, rehearsed on one: the cloud is split into the P slabs
+    lloyd.prepare would give P ranks (same histogram, owner table and stable
+    partition), each slab gets its own engine (pcm_layout_shard: global rows,
+    n_global), and every iteration runs iter_local on all P engines, sums their
+    statistics (standing in for the RCCL all-reduce) and runs iter_global on all
+    P.  HIP events around each engine's two launches give the per-rank cost of
+    an iteration without the collective.  The centres after the run are checked
+    against a single-engine fit of the whole cloud (bit-identical)."""
+    import torch
+
+    from pcm_amd import lloyd
+    from pcm_amd.engine import Engine, shard_hist, shard_partition, synth_rows, synth_uniform
+    from pcm_amd.fixed import fixed_q
+
+    torch.cuda.set_device(0)
+    N, K, D, P = args.n, args.k, args.d, args.slab_of
+    iters = args.warmup + args.steps
+    X = synth_uniform(N, D, seed=0)
+    C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0)
+    lo = X.min(0).values.double().cpu().numpy()
+    hi = X.max(0).values.double().cpu().numpy()
+    q = fixed_q(np.maximum(np.abs(lo), np.abs(hi)))
+    axis = int(np.argmax(hi - lo))
+    inv = lloyd.SLAB_BINS / (hi[axis] - lo[axis])
+    owner = lloyd.slab_owner(shard_hist(X, axis, lo[axis], inv, lloyd.SLAB_BINS).cpu().numpy(), P)
+    Xp, rows, cnt = shard_partition(X, axis, lo[axis], inv, lloyd.SLAB_BINS, owner, P, 0)
+    engines, off = [], 0
+    for r in range(P):
+        Xr, rr = Xp[off:off + int(cnt[r])], rows[off:off + int(cnt[r])]
+        off += int(cnt[r])
+        e = Engine(D, K, torch.float32, max_iter=iters + 4)
+        e.bbox(Xr)
+        e.set_shard(rr, N)
+        e.build(Xr, q, 0)
+        e.begin(C0, 0.0, iters + 4)
+        engines.append(e)
+    del Xp
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(P)]
+    t_assign = np.zeros(P)
+    t_step = np.zeros(P)
+
+    def step(timed):
+        for r, e in enumerate(engines):
+            if timed:
+                ev[r][0].record()
+            e.iter_local()
+            if timed:
+                ev[r][1].record()
+        total = engines[0].stats.clone()
+        for e in engines[1:]:
+            total += e.stats
+        for e in engines:
+            e.stats.copy_(total)
+        for r, e in enumerate(engines):
+            if timed:
+                ev[r][2].record()
+            e.iter_global()
+            if timed:
+                ev[r][3].record()
+        if timed:
+            torch.cuda.synchronize()
+            for r in range(P):
+                t_assign[r] += ev[r][0].elapsed_time(ev[r][1])
+                t_step[r] += ev[r][2].elapsed_time(ev[r][3])
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    for _ in range(args.steps):
+        step(True)
+    st = [e.status() for e in engines]
+    if any(s["halt"] or s["iter"] != iters for s in st):
+        raise SystemExit(f"slab proxy: iterations did not all run: {st[0]}")
+    C_slab = engines[0].centers().cpu().numpy()
+    ok = all(np.array_equal(C_slab, e.centers().cpu().numpy()) for e in engines)
+    info = [dict(e.layout_info(), points=int(e.n), kernel=e.assign_kernel(), **e.candidate_stats()) for e in engines]
+    del engines
+    one = Engine(D, K, torch.float32, max_iter=iters + 4)
+    lloyd.prepare(one, X, lloyd.LOCAL)
+    one.begin(C0, 0.0, iters + 4)
+    one.iterate(iters)
+    bitwise = ok and np.array_equal(C_slab, one.centers().cpu().numpy())
+    a_ms, s_ms = t_assign / args.steps, t_step / args.steps
+    per_rank = (a_ms + s_ms) * 1e3
+    return {"metric": "per-rank Lloyd iteration cost at P GPUs (1-GPU slab proxy, all-reduce excluded)",
+            "value": float(per_rank.max()), "unit": "us/iter (max over ranks)", "higher_is_better": False,
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "slab_of": P,
+            "config": {"workload": f"config 4 split {P} ways: N={N} K={K} D={D} fp32, slabs of axis {axis}"},
+            "per_rank_us": {"assign": (a_ms * 1e3).round(2).tolist(), "step": (s_ms * 1e3).round(2).tolist(),
+                            "total": per_rank.round(2).tolist()},
+            "slabs": info, "centres_bitwise_equal_single_engine": bool(bitwise)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -158,21 +292,62 @@ def main():
     ap.add_argument("--stereo", action="store_true", help="also time the stereo consistency gathers (4000x4000)")
     ap.add_argument("--cloud", action="store_true",
                     help="also time the per-pair cloud assembly (4000x4000 disparity) on GPU and CPU")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend at N > 1 (nccl = RCCL over xGMI; gloo: rehearsal of N ranks sharing "
+                         "one GPU, eager launches, host-staged collectives -- not a measurement)")
+    ap.add_argument("--shard", default="slab", choices=["slab", "rows"],
+                    help="N > 1: regroup the row shards into spatial slabs at layout time (default) or keep rows")
+    ap.add_argument("--slab-of", type=int, default=0, metavar="P",
+                    help="1-GPU proxy of config 4 at P GPUs: the P slab engines of lloyd.prepare's split run on this "
+                         "GPU, their statistics summed between the kernels (the all-reduce, emulated); per-rank "
+                         "k_lloyd1 + k_step times from HIP events (the per-rank iteration cost, RCCL excluded)")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launcher test: each rank prints its RANK/WORLD_SIZE as JSON and exits before any GPU call")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and env_world is None:
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        raise SystemExit(2)
+    if args.dry_launch:
+        print(json.dumps({"rank": rank, "local_rank": local, "world_size": world,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if args.slab_of > 1:
+        if world != 1:
+            raise SystemExit("--slab-of is a single-process proxy")
+        print(json.dumps(slab_proxy(args)), flush=True)
+        return
+
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > ndev:
+        print(f"bench.py: {world} ranks but {ndev} visible GPUs (RCCL needs one GPU per rank)", file=sys.stderr)
+        raise SystemExit(2)
+    dev_index = local % max(1, ndev)
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
+            raise SystemExit(2)
     elif args.split:
-        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29533", world_size=1, rank=0,
-                                device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", world_size=1, rank=0,
+                                device_id=torch.device("cuda", dev_index))
     multi = world > 1 or args.split
+    if world > 1 and args.backend == "gloo":
+        args.graph = False          # gloo collectives cannot be captured
 
     import pcm_amd
     from pcm_amd import lloyd
@@ -187,13 +362,12 @@ def main():
     total_iters = args.warmup + args.steps
     max_iter = total_iters + 16
     group = None
-
     eng = Engine(D, K, torch.float32, max_iter=max_iter)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    lloyd.prepare(eng, X, group)
+    lloyd.prepare(eng, X, group, args.shard)
     torch.cuda.synchronize()
     layout_ms = (time.perf_counter() - t0) * 1e3
     eng.begin(C0, 0.0, max_iter)
@@ -230,6 +404,10 @@ def main():
             graph = None
             args.graph_error = repr(exc)[:200]
             torch.cuda.synchronize()
+        # every rank replays (or every rank launches eagerly): collective sequences stay aligned
+        if not lloyd.agree(graph is not None, world, None, eng.stats_device):
+            graph = None
+            args.graph_error = getattr(args, "graph_error", None) or "capture failed on another rank"
         # capture recorded the launches without running them
         if eng.status()["iter"] != args.warmup:
             raise SystemExit("graph capture executed iterations")
@@ -299,7 +477,12 @@ def main():
         kpp_ms = (time.perf_counter() - t0) * 1e3
 
     if rank == 0:
-        n_local = hi_row - lo_row
+        n_local = int(eng.n)      # points this rank's engine holds (its slab at N > 1)
+        if world == 1:
+            workload = f"Lloyd K-means iteration, N={N} K={K} D={D} fp32 (config 3, 1 GPU)"
+        else:
+            workload = (f"Lloyd K-means iteration, N={N} K={K} D={D} fp32 (config 4, {world} GPUs, "
+                        f"{'spatial slabs' if args.shard == 'slab' else 'row shards'}, all-reduce every iteration)")
         # the iteration kernel streams only the points (labels are recomputed, not stored)
         bytes_pt = D * 4
         achieved = bytes_pt * n_local / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0
@@ -319,14 +502,17 @@ def main():
             "dtype": "f32",
             "data": "synthetic: counter-based U[0,1)^3 cloud generated on device (splitmix64), init = rows "
                     "sorted(default_rng(1).choice(N, K))",
-            "config": {"workload": f"Lloyd K-means iteration, N={N} K={K} D={D} fp32 "
-                                   f"({'config 3, 1 GPU' if world == 1 else f'config 4, row-sharded dp{world}'})",
-                       "n_points": N, "k": K, "d": D, "parallelism": f"row-shard dp{world}",
+            "config": {"workload": workload,
+                       "n_points": N, "k": K, "d": D,
+                       "parallelism": f"dp{world} ({'spatial slabs' if args.shard == 'slab' else 'row shards'})"
+                                      if world > 1 else "single GPU",
+                       "backend": (args.backend if world > 1 else ("nccl (group of 1)" if multi else None)),
                        "launch": "hip-graph" if graph is not None else "eager",
-                       "cells": info["ncells"], "tiles": info["ntiles"], "grid": info["grid"]},
+                       "cells": info["ncells"], "tiles": info["ntiles"], "grid": info["grid"],
+                       "rank0_points": n_local},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_lloyd1<float,3,8>",
+                         "kernel": eng.assign_kernel(),
                          "algorithmic_bytes_per_point": bytes_pt,
                          "avg_launch_ms": assign_ms, "timing": timing + ("" if world == 1 else " (max over ranks)")},
             "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"]},

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PCM_ABI_VERSION 2
+#define PCM_ABI_VERSION 3
 
 enum pcm_dtype { PCM_F32 = 0, PCM_F16 = 1, PCM_F64 = 2 /* dense path only */ };
 
@@ -102,6 +102,14 @@ int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream,
  * this call returns. */
 int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gidx0, void *stream);
 
+/* Layout, optional step between pcm_layout_bbox and pcm_layout_build: the
+ * engine's cloud is a SPATIAL shard of a fit over `n_global` points on all
+ * ranks (pcm_shard_* below).  `rows` (device uint32[n], copied) is each local
+ * point's global row index -- the relocation tie-break (distance desc, global
+ * row asc, _k_means_common.pyx:185-187) -- and n_global scales the pruning-grid
+ * policy (cells per centre) to the whole cloud.  Reset by pcm_layout_bbox. */
+int pcm_layout_shard(pcm_engine *e, const uint32_t *rows, int64_t n_global, void *stream);
+
 /* Start a fit from centres C0 (device, K*D float32): labels := -1, history
  * cleared, absolute shift tolerance `tol`, iteration cap `max_iter`. */
 int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void *stream);
@@ -150,6 +158,9 @@ int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream);
 
 /* Layout facts for diagnostics: cells, tiles, grid dims (host ints). */
 int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid /*[4]*/);
+/* Name of the assign-kernel variant the current layout launches per iteration
+ * (e.g. "k_lloyd1<float,3,8,false>"), for measurement records. */
+int pcm_assign_kernel_name(pcm_engine *e, char *buf, size_t n);
 /* Mean/max fine candidate-list length of the last iteration (synchronising). */
 int pcm_candidate_stats(pcm_engine *e, double *mean, int *max, int64_t *full_cells, void *stream);
 
@@ -174,6 +185,30 @@ int pcm_synth_uniform(float *out, int64_t n, int d, uint64_t seed, int64_t start
  * for centres C (device float32[K*D]).  q = fixed-point exponents. */
 int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int k,
                           const int32_t *q, int32_t *labels, uint64_t *stats, void *stream);
+
+/* ---------------------------------------------------------------- slab sharding
+ * Multi-GPU layout (no reference counterpart -- the reference is
+ * single-process): the row shards the ranks receive are regrouped into slabs
+ * of the longest axis so that each rank's pruning grid covers only its slab.
+ * X: device n*d rows (dtype PCM_F32/PCM_F16) whose global row index is gidx0 + i.
+ * bin(x) = clamp(floor((x[axis] - lo) * inv), 0, nbins - 1), computed in fp64.
+ *   pcm_shard_hist       hist[nbins] (device uint64, overwritten), nbins <= 16384;
+ *   pcm_shard_partition  stable partition by owner[bin] (device uint8[nbins],
+ *                        values < P): X_out (device n*d) holds the rows grouped
+ *                        by destination rank in original order, rows_out
+ *                        (device uint32[n]) their global indices, counts (host
+ *                        int64[P]) the group sizes; synchronises `stream`;
+ *   pcm_shard_scatter_labels  out[rows[i] - gidx0] = labels[i] (device int32):
+ *                        labels returned in the partition's order -> row order. */
+#define PCM_SHARD_MAXP 16
+int pcm_shard_hist(const void *X, int dtype, int64_t n, int d, int axis, double lo, double inv, int nbins,
+                   uint64_t *hist, void *stream);
+int pcm_shard_partition_workspace(int64_t n, int P, size_t *bytes);
+int pcm_shard_partition(const void *X, int dtype, int64_t n, int d, int axis, double lo, double inv, int nbins,
+                        const uint8_t *owner, int P, int64_t gidx0, void *X_out, uint32_t *rows_out, int64_t *counts,
+                        void *workspace, size_t workspace_bytes, void *stream);
+int pcm_shard_scatter_labels(const int32_t *labels, const uint32_t *rows, int64_t n, int64_t gidx0, int32_t *out,
+                             void *stream);
 
 /* k-means++ seeding, replacing scikit-learn's _kmeans_plusplus
  * (sklearn/cluster/_kmeans.py:174-272; KMeans' default init, :1012-1019; the

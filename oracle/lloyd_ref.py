@@ -178,7 +178,8 @@ def far_candidates(X, C, labels, gidx0: int, m: int, weights=None):
     (dist desc, global index asc).  ``_k_means_common.pyx:185-187``.
     """
     dist = sqdist_rows(X, C[labels])
-    gidx = np.arange(X.shape[0], dtype=np.int64) + gidx0
+    # gidx0: the global row of local row 0 (row shard), or every local row's global row (spatial shard)
+    gidx = np.asarray(gidx0, np.int64) if np.ndim(gidx0) else np.arange(X.shape[0], dtype=np.int64) + gidx0
     order = np.lexsort((gidx, -dist.astype(np.float64)))[:m]
     w = np.ones(X.shape[0], dtype=np.int64) if weights is None else np.asarray(weights, dtype=np.int64)
     return dist[order], gidx[order], labels[order], X[order], w[order]

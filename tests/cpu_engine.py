@@ -24,6 +24,7 @@ class OracleEngine:
 
     # ---------------- layout
     def bbox(self, X):
+        self.rows = None
         self.X = np.ascontiguousarray(X.cpu().numpy(), dtype=np.float32)
         self.n = self.X.shape[0]
         if self.n == 0:
@@ -34,8 +35,34 @@ class OracleEngine:
 
     def build(self, X, q, gidx0=0):
         self.q = np.asarray(q, dtype=np.int32)
-        self.gidx0 = int(gidx0)
+        if getattr(self, "rows", None) is None:
+            self.gidx0 = int(gidx0)
         self.stats = torch.zeros(self.k * (self.d + 1) + 1, dtype=torch.int64)
+
+    # ---------------- spatial slab sharding (numpy restatement of csrc/pcm_shard.hip)
+    def set_shard(self, rows, n_global):
+        self.rows = rows.numpy().astype(np.uint32).astype(np.int64)
+        self.gidx0 = self.rows              # far_candidates takes the per-row global index
+
+    @staticmethod
+    def _bins(X, axis, lo, inv, nbins):
+        x = np.ascontiguousarray(X.cpu().numpy())[:, axis].astype(np.float32).astype(np.float64)
+        return np.clip(np.floor((x - lo) * inv), 0, nbins - 1).astype(np.int64)
+
+    def shard_hist(self, X, axis, lo, inv, nbins):
+        return torch.from_numpy(np.bincount(self._bins(X, axis, lo, inv, nbins), minlength=nbins).astype(np.int64))
+
+    def shard_partition(self, X, axis, lo, inv, nbins, owner, world, gidx0):
+        dest = np.asarray(owner, np.int64)[self._bins(X, axis, lo, inv, nbins)]
+        order = np.argsort(dest, kind="stable")
+        counts = np.bincount(dest, minlength=world).astype(np.int64)
+        rows = (order + int(gidx0)).astype(np.int64).astype(np.int32)
+        return X[torch.from_numpy(order)].contiguous(), torch.from_numpy(rows), counts
+
+    def shard_scatter_labels(self, labels, rows, gidx0, n):
+        out = np.empty(n, np.int32)
+        out[rows.numpy().astype(np.uint32).astype(np.int64) - int(gidx0)] = labels.numpy()
+        return torch.from_numpy(out)
 
     # ---------------- iterations
     def begin(self, C0, tol, max_iter):

@@ -62,11 +62,19 @@ class SyntheticStages:
     (disparity, validity mask, photoconsistency, debug image layers) of the
     shape the reference's disparity_map returns (disparity.py:21-226)."""
 
-    def __init__(self, n_pairs=2, shape=(120, 160), seed=0, fail_at=None):
-        self.n_pairs, self.shape, self.seed, self.fail_at = n_pairs, shape, seed, fail_at
+    def __init__(self, n_pairs=2, shape=(120, 160), seed=0, fail_at=None, fail=None):
+        self.n_pairs, self.shape, self.seed, self.fail_at, self.fail = n_pairs, shape, seed, fail_at, fail
+        self.logged = []
+
+    def log(self, msg):
+        self.logged.append(msg)
 
     def pairs(self, kml_path, is_debug_mode=True, is_debug_pair=False, is_one_random_pair=True, n=10):
-        from pcm_amd.pipeline import PairProducts
+        from pcm_amd.pipeline import CropFailed, ImageNotFound, PairProducts
+        if self.fail == "image":
+            raise ImageNotFound("/data/WV3/PAN/missing.NTF")
+        if self.fail == "crop":
+            raise CropFailed("KML region outside the image")
         rng = np.random.default_rng(self.seed)
         H, W = self.shape
         yy, xx = np.mgrid[0:H, 0:W]

@@ -28,7 +28,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False):
+def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False, shard="auto"):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -40,27 +40,30 @@ def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False):
     a, b = (0, n) if local else (n * rank // world, n * (rank + 1) // world)
     eng = OracleEngine(X.shape[1], C0.shape[0], max_iter)
     res = pcm_amd.lloyd_fit(torch.from_numpy(X[a:b]), torch.from_numpy(C0), max_iter=max_iter, tol=0.0,
-                            chunk=chunk, engine=eng, group=LOCAL if local else None)
+                            chunk=chunk, engine=eng, group=LOCAL if local else None, shard=shard)
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), labels=res.labels.numpy(), centers=res.centers.numpy(),
-             n_iter=res.n_iter, inertia=res.inertia, changed=res.changed, relocs=res.relocations)
+             n_iter=res.n_iter, inertia=res.inertia, changed=res.changed, relocs=res.relocations,
+             shard=res.layout.get("shard", "rows"), slab_points=res.layout.get("slab_points", -1))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def run_world(X, C0, max_iter, chunk, tmp_path, world=2, local=False):
+def run_world(X, C0, max_iter, chunk, tmp_path, world=2, local=False, shard="auto"):
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, X, C0, max_iter, chunk, str(tmp_path), local), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, X, C0, max_iter, chunk, str(tmp_path), local, shard), nprocs=world,
+             join=True)
     parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
     return parts
 
 
-@pytest.mark.parametrize("chunk", [1, 4])
-def test_two_ranks_match_single_process(tmp_path, chunk):
+@pytest.mark.parametrize("chunk,shard", [(1, "slab"), (4, "slab"), (4, "rows")])
+def test_two_ranks_match_single_process(tmp_path, chunk, shard):
     from oracle import lloyd_ref as R
     X = R.splitmix_uniform(6000, 3, 21)
     C0 = X[R.init_indices(6000, 24)]
     ref = R.lloyd_fit(X, C0, max_iter=15)
-    parts = run_world(X, C0, 15, chunk, tmp_path)
+    parts = run_world(X, C0, 15, chunk, tmp_path, shard=shard)
+    assert all(str(p["shard"]) == shard for p in parts)
     labels = np.concatenate([p["labels"] for p in parts])
     np.testing.assert_array_equal(labels, ref["labels"])
     for p in parts:
@@ -71,7 +74,8 @@ def test_two_ranks_match_single_process(tmp_path, chunk):
         assert float(p["inertia"]) == ref["inertia"]
 
 
-def test_two_ranks_relocation(tmp_path):
+@pytest.mark.parametrize("shard", ["slab", "rows"])
+def test_two_ranks_relocation(tmp_path, shard):
     """Empty clusters whose farthest points live on different ranks."""
     from oracle import lloyd_ref as R
     X = R.splitmix_uniform(3000, 3, 22)
@@ -79,7 +83,7 @@ def test_two_ranks_relocation(tmp_path):
     X[2900] = [-2.0, 4.0, 1.0]
     C0 = np.concatenate([X[:6], np.array([[50, 50, 50], [60, 60, 60], [70, 70, 70]], np.float32)])
     ref = R.lloyd_fit(X, C0, max_iter=20)
-    parts = run_world(X, C0, 20, 3, tmp_path)
+    parts = run_world(X, C0, 20, 3, tmp_path, shard=shard)
     labels = np.concatenate([p["labels"] for p in parts])
     assert int(parts[0]["relocs"]) >= 1
     np.testing.assert_array_equal(labels, ref["labels"])
@@ -99,4 +103,39 @@ def test_local_group_under_default_group(tmp_path):
     for p in parts:
         np.testing.assert_array_equal(p["labels"], ref["labels"])
         np.testing.assert_array_equal(p["centers"], ref["centers"])
+        assert float(p["inertia"]) == ref["inertia"]
+
+
+def test_slab_owner_equal_count_contiguous():
+    from pcm_amd.lloyd import slab_owner
+    rng = np.random.default_rng(0)
+    h = rng.integers(0, 50, 1000)
+    for world in (1, 2, 3, 8):
+        own = slab_owner(h, world)
+        assert own.dtype == np.uint8 and own.min() >= 0 and own.max() <= world - 1
+        assert np.all(np.diff(own.astype(int)) >= 0)                       # contiguous slabs
+        per = np.bincount(own, weights=h, minlength=world)
+        assert np.all(np.abs(per - h.sum() / world) <= h.max())            # equal count up to one bin
+    assert np.all(slab_owner(np.zeros(10, np.int64), 4) == 0)
+
+
+def test_three_ranks_skewed_slabs(tmp_path):
+    """Skewed cloud (most points in one corner, a few far away, duplicates): the
+    equal-count slabs are very unequal in width, some bins are empty, a rank's
+    row shard sends most of its rows elsewhere -- labels still come back in each
+    rank's row order, bit-identical to the single-process fit."""
+    from oracle import lloyd_ref as R
+    X = R.splitmix_uniform(5000, 3, 24)
+    X[:4000] *= np.float32(0.01)
+    X[4000:4100] = X[4000]                    # exact duplicates
+    X[4990:] += np.float32(40.0)
+    C0 = X[R.init_indices(5000, 16)]
+    ref = R.lloyd_fit(X, C0, max_iter=12)
+    parts = run_world(X, C0, 12, 3, tmp_path, world=3)
+    labels = np.concatenate([p["labels"] for p in parts])
+    np.testing.assert_array_equal(labels, ref["labels"])
+    assert sum(int(p["slab_points"]) for p in parts) == 5000
+    for p in parts:
+        np.testing.assert_array_equal(p["centers"], ref["centers"])
+        assert int(p["n_iter"]) == ref["n_iter"]
         assert float(p["inertia"]) == ref["inertia"]

@@ -32,7 +32,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, X, C0, max_iter, chunk, dtype, out_dir):
+def _worker(rank, world, port, X, C0, max_iter, chunk, dtype, out_dir, shard):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -42,18 +42,18 @@ def _worker(rank, world, port, X, C0, max_iter, chunk, dtype, out_dir):
     n = X.shape[0]
     a, b = n * rank // world, n * (rank + 1) // world
     Xs = torch.from_numpy(np.ascontiguousarray(X[a:b])).to("cuda", dtype)
-    res = pcm_amd.lloyd_fit(Xs, torch.from_numpy(C0).cuda(), max_iter=max_iter, tol=0.0, chunk=chunk)
+    res = pcm_amd.lloyd_fit(Xs, torch.from_numpy(C0).cuda(), max_iter=max_iter, tol=0.0, chunk=chunk, shard=shard)
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), labels=res.labels.cpu().numpy(),
              centers=res.centers.cpu().numpy(), n_iter=res.n_iter, inertia=res.inertia, changed=res.changed,
-             relocs=res.relocations)
+             relocs=res.relocations, shard=res.layout["shard"], slab_points=res.layout.get("slab_points", -1))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def run_world(X, C0, max_iter, chunk, tmp_path, world=2, dtype=torch.float32):
+def run_world(X, C0, max_iter, chunk, tmp_path, world=2, dtype=torch.float32, shard="auto"):
     import torch.multiprocessing as mp
-    mp.spawn(_worker, args=(world, _free_port(), X, C0, max_iter, chunk, dtype, str(tmp_path)), nprocs=world,
+    mp.spawn(_worker, args=(world, _free_port(), X, C0, max_iter, chunk, dtype, str(tmp_path), shard), nprocs=world,
              join=True)
     return [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
 
@@ -85,12 +85,13 @@ def compare(parts, res1, ref):
         assert float(p["inertia"]) == ref["inertia"] == res1.inertia   # exact limbs, all-reduced
 
 
-@pytest.mark.parametrize("chunk", [1, 5])
-def test_two_ranks_hip_engine(pcm, tmp_path, chunk):
+@pytest.mark.parametrize("chunk,shard", [(1, "slab"), (5, "slab"), (5, "rows")])
+def test_two_ranks_hip_engine(pcm, tmp_path, chunk, shard):
     X = R.splitmix_uniform(300_000, 3, 41)
     C0 = X[R.init_indices(300_000, 256)]
     ref = R.lloyd_fit(X, C0, max_iter=12, fast=True)
-    parts = run_world(X, C0, 12, chunk, tmp_path)
+    parts = run_world(X, C0, 12, chunk, tmp_path, shard=shard)
+    assert all(str(p["shard"]) == shard for p in parts)
     compare(parts, single(pcm, X, C0, 12), ref)
 
 
@@ -102,14 +103,30 @@ def test_two_ranks_hip_engine_fp16_d4(pcm, tmp_path):
     compare(parts, single(pcm, X, C0, 8, torch.float16), ref)
 
 
-def test_two_ranks_hip_relocation_across_shards(pcm, tmp_path):
-    """Empty clusters whose farthest points sit on different ranks."""
+@pytest.mark.parametrize("shard", ["slab", "rows"])
+def test_two_ranks_hip_relocation_across_shards(pcm, tmp_path, shard):
+    """Empty clusters whose farthest points sit on different ranks (slabs: the
+    relocation tie-break uses the global rows carried by pcm_layout_shard)."""
     X = R.splitmix_uniform(40_000, 3, 43)
     X[1_000] = [3.0, 3.0, 3.0]           # rank 0's far outlier
     X[39_000] = [-2.0, 4.0, 1.0]         # rank 1's (farther)
     X[25_000] = [2.5, -1.5, 2.0]         # rank 1
     C0 = np.concatenate([X[:20], np.array([[50, 50, 50], [60, 60, 60], [70, 70, 70]], np.float32)])
     ref = R.lloyd_fit(X, C0, max_iter=20, fast=True)
-    parts = run_world(X, C0, 20, 3, tmp_path)
+    parts = run_world(X, C0, 20, 3, tmp_path, shard=shard)
     assert int(parts[0]["relocs"]) >= 1 and int(parts[1]["relocs"]) == int(parts[0]["relocs"])
     compare(parts, single(pcm, X, C0, 20), ref)
+
+
+def test_three_ranks_hip_skewed_slabs(pcm, tmp_path):
+    """Three ranks, skewed cloud with duplicates and far points: very unequal slab
+    widths and a rank whose rows mostly move away; bit-identical to the oracle."""
+    X = R.splitmix_uniform(90_000, 3, 44)
+    X[:70_000] *= np.float32(0.01)
+    X[70_000:72_000] = X[70_000]
+    X[89_900:] += np.float32(40.0)
+    C0 = X[R.init_indices(90_000, 64)]
+    ref = R.lloyd_fit(X, C0, max_iter=10, fast=True)
+    parts = run_world(X, C0, 10, 4, tmp_path, world=3)
+    assert sum(int(p["slab_points"]) for p in parts) == 90_000
+    compare(parts, single(pcm, X, C0, 10), ref)

@@ -118,6 +118,28 @@ def test_stages_error_becomes_error_layer():
     assert len(out) == 1 and out[0][1]["name"] == "Error: synthetic stereo failure"
 
 
+def test_reference_error_layers():
+    """plugin.py:77-79 / 89-91: a missing image and a failed crop return np.zeros((100, 100))
+    named "error: image not found" / "error: <msg>"; other failures np.ones named "Error: <msg>"."""
+    from fake_pipeline import SyntheticStages
+    out = pcm_amd.HeightMapExtractor(stages=SyntheticStages(fail="image"), fit=oracle_fit).run("roi.kml")
+    assert len(out) == 1 and out[0][1] == {"name": "error: image not found"} and out[0][2] == "image"
+    assert out[0][0].shape == (100, 100) and not out[0][0].any()
+    out = pcm_amd.HeightMapExtractor(stages=SyntheticStages(fail="crop"), fit=oracle_fit).run("roi.kml")
+    assert out[0][1] == {"name": "error: KML region outside the image"} and not out[0][0].any()
+    st = SyntheticStages(fail_at=0)
+    out = pcm_amd.HeightMapExtractor(stages=st, fit=oracle_fit, _assemble=oracle_assemble).run("roi.kml")
+    assert out[0][1] == {"name": "Error: synthetic stereo failure"} and out[0][0].shape == (100, 100)
+    assert (out[0][0] == 1).all() and st.logged[-1].startswith("Error: synthetic stereo failure")
+
+
+def test_stages_log_added_layers():
+    from fake_pipeline import SyntheticStages
+    st = SyntheticStages(n_pairs=1, shape=(40, 50))
+    layers = pcm_amd.HeightMapExtractor(stages=st, n_clusters=4, fit=oracle_fit, _assemble=oracle_assemble).run("k")
+    assert st.logged == [f"Added {len(layers)} layers to Napari"]    # plugin.py:234
+
+
 @pytest.mark.gpu
 def test_gpu_stages_path_device_fusion():
     """GPU cloud assembly on the plugin path (no host round trip into the K-means):
