@@ -114,6 +114,8 @@ def dense_kmeanspp(X: torch.Tensor, n_clusters: int, *, random_state=None, n_loc
     k = int(n_clusters)
     if not 1 <= k <= n:
         raise ValueError(f"n_samples={n} should be >= n_clusters={k}")
+    if not torch.isfinite(X).all():      # before any weight is formed (kmeans_plusplus raises likewise)
+        raise ValueError("input points contain NaN or Inf")
     rs = random_state if isinstance(random_state, np.random.RandomState) else np.random.RandomState(random_state)
     L = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
     u0 = rs.random_sample()
@@ -129,7 +131,9 @@ def dense_kmeanspp(X: torch.Tensor, n_clusters: int, *, random_state=None, n_loc
     _lib.check(lib.pcm_dense_kmeanspp_workspace(n, d, _dtype_code(X), k, L, ctypes.byref(nbytes)),
                "pcm_dense_kmeanspp_workspace")
     ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=X.device)
-    _lib.check(lib.pcm_dense_kmeanspp(_ptr(X), n, d, _dtype_code(X), k, L, _first_index(n, u0),
+    # sklearn's unit sample weights are in X's dtype: the first draw follows numpy's choice() for it
+    first = _first_index(n, u0, np.float64 if X.dtype == torch.float64 else np.float32)
+    _lib.check(lib.pcm_dense_kmeanspp(_ptr(X), n, d, _dtype_code(X), k, L, first,
                                       umant.ctypes.data_as(ctypes.c_void_p), s, _ptr(idx), _ptr(ws), nbytes.value,
                                       _stream()), "pcm_dense_kmeanspp")
     return X[idx].clone(), idx

@@ -22,8 +22,14 @@ the boundary, which mirror sklearn's own NumPy calls.  Dtypes follow sklearn
 
 * float32 point clouds (D <= 4): the pruned point-cloud engine (``lloyd_fit``,
   ``kmeans_plusplus``; canonical float32 arithmetic, DESIGN.md §2);
-* float64 input or D > 4 (the reference's 1500 x 20 float64 call site): the
-  dense engine (``dense.py``), computing in the input precision.
+* D > 4, or float64 input the dense engine can take (the reference's
+  1500 x 20 float64 call site): the dense engine (``dense.py``), computing in the
+  input precision;
+* float64 point clouds (D <= 4) too large for the dense engine -- centres
+  beyond its 64 KB LDS stage (K * D * 8 bytes) or more than 2**26 distance
+  evaluations per iteration (N * K) -- go to the pruned engine in float32 (the
+  boundary cast of the plugin path; its canonical fp32 fit equals sklearn's
+  float64 fit on pixel-unit height-map clouds, tests/test_plugin_cloud_golden.py).
 """
 from __future__ import annotations
 
@@ -57,21 +63,31 @@ class KMeans:
         self._seed = _seed    # tests: a CPU stand-in for k-means++ (Xc, k, RandomState) -> centers
 
     # ------------------------------------------------------------ GPU legs
+    DENSE_LDS_BYTES = 64 * 1024        # the dense engine stages all K centres in LDS (pcm_dense.hip)
+    DENSE_MAX_EVALS = 1 << 26          # N * K distance evaluations per brute-force iteration
+
     @staticmethod
-    def _dense(X: np.ndarray) -> bool:
-        return X.dtype == np.float64 or X.shape[1] > 4
+    def _dense(X: np.ndarray, k: int) -> bool:
+        """Which engine fits X with k clusters: True = dense (input precision), False = pruned (float32)."""
+        n, d = X.shape
+        if d > 4:
+            return True
+        if X.dtype != np.float64:
+            return False
+        return k * d * 8 <= KMeans.DENSE_LDS_BYTES and n * k <= KMeans.DENSE_MAX_EVALS
 
     @staticmethod
     def _gpu_fit(Xc: np.ndarray, C0: np.ndarray, max_iter: int, tol: float):
         import torch
 
-        if KMeans._dense(Xc):
+        if KMeans._dense(Xc, C0.shape[0]):
             from .dense import dense_fit
             res = dense_fit(torch.from_numpy(Xc).cuda(), torch.from_numpy(np.ascontiguousarray(C0, Xc.dtype)).cuda(),
                             max_iter=max_iter, tol=tol)
         else:
             from .lloyd import LOCAL, lloyd_fit
-            res = lloyd_fit(torch.from_numpy(Xc).cuda(), torch.from_numpy(np.ascontiguousarray(C0, np.float32)).cuda(),
+            Xf = np.ascontiguousarray(Xc, np.float32)
+            res = lloyd_fit(torch.from_numpy(Xf).cuda(), torch.from_numpy(np.ascontiguousarray(C0, np.float32)).cuda(),
                             max_iter=max_iter, tol=tol, group=LOCAL)
         torch.cuda.synchronize()
         return res.labels.cpu().numpy(), res.centers.cpu().numpy(), float(res.inertia), int(res.n_iter)
@@ -80,13 +96,13 @@ class KMeans:
     def _gpu_seed(Xc: np.ndarray, k: int, rs: np.random.RandomState) -> np.ndarray:
         import torch
 
-        if KMeans._dense(Xc):
+        if KMeans._dense(Xc, k):
             from .dense import dense_kmeanspp
             C, _ = dense_kmeanspp(torch.from_numpy(Xc).cuda(), k, random_state=rs)
         else:
             from .kpp import kmeans_plusplus
-            C, _ = kmeans_plusplus(torch.from_numpy(Xc).cuda(), k, random_state=rs)
-        return C.cpu().numpy()
+            C, _ = kmeans_plusplus(torch.from_numpy(np.ascontiguousarray(Xc, np.float32)).cuda(), k, random_state=rs)
+        return C.cpu().numpy().astype(Xc.dtype)
 
     # ------------------------------------------------------------ sklearn API
     def fit(self, X, y=None, sample_weight=None):
@@ -99,6 +115,10 @@ class KMeans:
         X = np.asarray(X)
         dt = np.float32 if X.dtype == np.float32 else np.float64     # sklearn: dtype=[float64, float32]
         X = np.array(X, dtype=dt, order="C", copy=True)
+        if X.ndim != 2:
+            raise ValueError("Expected a 2D array")
+        if not np.isfinite(X).all():                                      # sklearn check_array
+            raise ValueError("Input X contains NaN or infinity.")
         n, d = X.shape
         k = int(self.n_clusters)
         if n < k:

@@ -29,15 +29,24 @@ def _scale(n: int, maxd: float) -> int:
     return int(62 - max(1, int(n - 1).bit_length()) - e)
 
 
-def _first_index(n: int, u0: float) -> int:
+def _first_index(n: int, u0: float, weight_dtype=np.float32) -> int:
     """numpy RandomState.choice(n, p=w / w.sum()) for its single random_sample() draw u0,
-    with sklearn's unit float32 weights (``_check_sample_weight`` in X's dtype).
+    with sklearn's unit weights in X's dtype (``_check_sample_weight``).
 
-    choice() searches u0 (side='right') in cdf = cumsum(p) / cumsum(p)[-1] with
-    p[i] = v (one float32 constant widened to float64).  For n < 2**29 every
-    partial sum (i + 1) * v is exact in float64 (v has 24 significant bits), so
-    cdf[i] = RN((i + 1) / n) whatever v is: the index is the first i with
-    RN((i + 1) / n) > u0 -- O(1) instead of three n-element float64 arrays."""
+    choice() searches u0 (side='right') in cdf = cumsum(p) / cumsum(p)[-1].
+    float32 weights: p[i] = v (one float32 constant widened to float64); for
+    n < 2**29 every partial sum (i + 1) * v is exact in float64 (v has 24
+    significant bits), so cdf[i] = RN((i + 1) / n) whatever v is: the index is
+    the first i with RN((i + 1) / n) > u0 -- O(1) instead of three n-element
+    float64 arrays.  float64 weights: p[i] = RN(1/n) and the float64 cumsum
+    rounds, so numpy's arithmetic is replayed (host bookkeeping of the random
+    stream, O(n))."""
+    if np.dtype(weight_dtype) == np.float64:
+        w = np.ones(n, dtype=np.float64)
+        p = w / w.sum()
+        cdf = p.cumsum()
+        cdf /= cdf[-1]
+        return int(cdf.searchsorted(u0, side="right"))
     if n >= 2 ** 29:
         w = np.ones(n, dtype=np.float32)
         p = (w / w.sum()).astype(np.float64)

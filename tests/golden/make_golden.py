@@ -25,6 +25,14 @@ Fixtures (all float32, unit weights, n_threads=1):
                      one _kmeans_single_lloyd run from X[:5] (float64) and the
                      kmeans_plusplus indices of random_state=42.
   dense_d8_f32.npz   600 x 8 float32, K=6: _kmeans_single_lloyd from X[:6].
+  plugin/plugin_cloud_k{64,16}.npz  the cloud shape the plugin emits
+                     (plugin.py:147-192): 65,917 points, pixel-unit y in
+                     [0, 1500), x in [0, 2200), z = relative height shifted so
+                     its 2nd percentile is 0 (negative below), float32 at the
+                     boundary; k-means++ init (random_state 0 / 1); sklearn's
+                     float64 Lloyd (the reference's dtype, plugin.py:192): a
+                     tol=0 fit, a tol=1e-4 fit (_tolerance) and 5 steps; plus
+                     the float32 sklearn fit.
 """
 import os
 
@@ -101,42 +109,61 @@ def main():
 
     jasraj()
     dense_f32()
+    plugin_cloud()
 
 
-def obia_features(n=1500, d=20, seed=42):
-    """Superpixel-feature-like rows (LAB means/stds, Gabor energies, entropy:
-    mixed scales and correlated groups), 7 land-cover classes."""
-    rng = np.random.default_rng(seed)
-    proto = rng.normal(0, 1, (7, d)) * rng.uniform(0.5, 3.0, d) + rng.uniform(-5, 50, d)
-    cls = rng.integers(0, 7, n)
-    X = proto[cls] + rng.normal(0, 1, (n, d)) * rng.uniform(0.3, 2.0, d)
-    X[:, 3:6] = np.abs(X[:, 3:6])                     # std-like features
-    X[:, -1] = np.log1p(np.abs(X[:, -1]))             # entropy-like
-    return X.astype(np.float64)
-
-
-def jasraj():
-    from sklearn.cluster import KMeans, kmeans_plusplus
-    from sklearn.preprocessing import StandardScaler
-    Xs = StandardScaler().fit_transform(obia_features())          # core.py:225-226
-    km = KMeans(n_clusters=5, random_state=42, n_init=10).fit(Xs)  # core.py:227-228
-    w = np.ones(Xs.shape[0])
-    lab1, in1, cen1, it1 = _kmeans_single_lloyd(Xs, w, Xs[:5].copy(), max_iter=300, tol=0.0, n_threads=1)
-    _, kidx = kmeans_plusplus(Xs, 5, random_state=42)
-    d = dict(X=Xs, labels=km.labels_.astype(np.int32), centers=km.cluster_centers_, inertia=np.float64(km.inertia_),
-             n_iter=np.int64(km.n_iter_), single_labels=lab1, single_centers=cen1, single_inertia=np.float64(in1),
-             single_n_iter=np.int64(it1), kpp_indices=kidx.astype(np.int64))
-    np.savez_compressed(os.path.join(OUT_DENSE, "jasraj_obia_k5.npz"), **d)
-    print("jasraj_obia_k5.npz", {k: v.shape for k, v in d.items()})
-
-
-def dense_f32():
-    X = obia_features(600, 8, seed=3).astype(np.float32)
-    w = np.ones(X.shape[0], dtype=np.float32)
-    lab, ine, cen, it = _kmeans_single_lloyd(X, w, X[:6].copy(), max_iter=300, tol=0.0, n_threads=1)
-    d = dict(X=X, C0=X[:6].copy(), fit_labels=lab, fit_centers=cen, fit_inertia=np.float64(ine), fit_n_iter=np.int64(it))
-    np.savez_compressed(os.path.join(OUT_DENSE, "dense_d8_f32.npz"), **d)
-    print("dense_d8_f32.npz", {k: v.shape for k, v in d.items()})
+def plugin_cloud():
+    """Pixel-unit height-map cloud as plugin.py:147-192 emits it (restated by
+    tests/fake_pipeline.pair_cloud): sparse valid pixels of a 1500 x 2200
+    disparity map.  The reference's points are float64 (plugin.py:192) and
+    scikit-learn keeps the input dtype, so the reference CPU path on this cloud
+    is the float64 Lloyd on the (float32-cast) points; the float32 sklearn fit
+    of the same points is recorded too (its GEMM-form rounding at pixel scale
+    takes another trajectory: see DESIGN.md §2)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(OUT))
+    from fake_pipeline import pair_cloud
+    from sklearn.cluster import kmeans_plusplus
+    from sklearn.cluster._kmeans import _tolerance
+    H, W = 1500, 2200
+    rng = np.random.default_rng(7)
+    yy, xx = np.mgrid[0:H, 0:W]
+    disparity = -16.0 * (8 * np.sin(xx / 230.0) + 5 * np.cos(yy / 170.0) + 0.002 * xx + rng.normal(0, 0.3, (H, W)))
+    height_map = -disparity / 16.0
+    valid = rng.random((H, W)) < 0.02
+    pts, _ = pair_cloud(height_map, valid)
+    X = pts.astype(np.float32)                     # the GPU boundary cast (SURVEY.md a4)
+    X64 = X.astype(np.float64)
+    for K, seed in ((64, 0), (16, 1)):
+        C0 = kmeans_plusplus(X64, K, random_state=seed)[0].astype(np.float32)
+        w64 = np.ones(X.shape[0])
+        d = dict(X=X, C0=C0)
+        lab, ine, cen, it = _kmeans_single_lloyd(X64, w64, C0.astype(np.float64), max_iter=300, tol=0.0, n_threads=1)
+        d.update(f64_labels=lab, f64_centers=cen, f64_inertia=np.float64(ine), f64_n_iter=np.int64(it))
+        tol = _tolerance(X64, 1e-4)
+        lab, ine, cen, it = _kmeans_single_lloyd(X64, w64, C0.astype(np.float64), max_iter=300, tol=tol, n_threads=1)
+        d.update(tol_abs=np.float64(tol), tol_labels=lab, tol_centers=cen, tol_inertia=np.float64(ine),
+                 tol_n_iter=np.int64(it))
+        lab, ine, cen, it = _kmeans_single_lloyd(X, np.ones(X.shape[0], np.float32), C0.copy(), max_iter=300,
+                                                 tol=0.0, n_threads=1)
+        d.update(f32_labels=lab, f32_centers=cen, f32_inertia=np.float64(ine), f32_n_iter=np.int64(it))
+        # float64 steps from C0 (E-step labels, counts, new centres) via lloyd_iter_chunked_dense
+        C = C0.astype(np.float64)
+        rec = dict(step_c_in=[], step_labels=[], step_c_out=[], step_weight=[])
+        for _ in range(5):
+            Cn = np.zeros_like(C)
+            wic = np.zeros(K)
+            lb = np.full(X.shape[0], -1, dtype=np.int32)
+            lloyd_iter_chunked_dense(X64, w64, C, Cn, wic, lb, np.zeros(K), 1)
+            rec["step_c_in"].append(C.copy())
+            rec["step_labels"].append(lb)
+            rec["step_c_out"].append(Cn.copy())
+            rec["step_weight"].append(wic.copy())
+            C = Cn
+        d.update({k_: np.stack(v) for k_, v in rec.items()})
+        name = f"plugin_cloud_k{K}.npz"
+        np.savez_compressed(os.path.join(OUT, "plugin", name), **d)
+        print(name, {k: v.shape for k, v in d.items()})
 
 
 if __name__ == "__main__":

@@ -174,3 +174,68 @@ def test_gpu_estimator_call_site(gpu):
     ref = pcm.KMeans(n_clusters=5, random_state=42, n_init=10, _fit=oracle_fit, _seed=oracle_seed).fit(g["X"])
     np.testing.assert_array_equal(est.cluster_centers_, ref.cluster_centers_)
     assert est.inertia_ == ref.inertia_
+
+
+# ---------------------------------------------------------------- ADVICE r2 (routing, first draw, NaN)
+def test_first_index_matches_numpy_choice_float64_and_float32():
+    """kpp._first_index replays RandomState.choice(n, p=w / w.sum()) for sklearn's unit
+    weights in X's dtype (float64 weights: the rounded cumsum is replayed)."""
+    from pcm_amd.kpp import _first_index
+    for n in (1, 2, 3, 7, 1500, 4097, 100_003):
+        for seed in range(12):
+            for dt in (np.float32, np.float64):
+                rs = np.random.RandomState(seed)
+                w = np.ones(n, dtype=dt)
+                want = rs.choice(n, p=w / w.sum())
+                u0 = np.random.RandomState(seed).random_sample()
+                assert _first_index(n, u0, dt) == want, (n, seed, dt)
+
+
+def test_estimator_engine_routing():
+    from pcm_amd.estimator import KMeans
+    f64, f32 = np.zeros((1500, 20)), np.zeros((1500, 3), np.float32)
+    assert KMeans._dense(f64, 5)                                    # the call site: dense, float64
+    assert KMeans._dense(np.zeros((1000, 3)), 8)                    # small float64 cloud: dense
+    assert not KMeans._dense(f32, 8)                                # float32 cloud: pruned engine
+    assert not KMeans._dense(np.zeros((1000, 3)), 4096)             # K*D*8 > 64 KB: pruned (float32)
+    assert not KMeans._dense(np.zeros((200_000, 4)), 1024)          # N*K > 2^26: pruned
+    assert KMeans._dense(np.zeros((10, 5), np.float32), 3)          # D > 4: dense whatever the dtype
+
+
+def test_estimator_rejects_nonfinite_before_any_device_call():
+    from pcm_amd.estimator import KMeans
+
+    def never(*a, **k):
+        raise AssertionError("must not be reached")
+    X = np.random.default_rng(0).random((100, 3))
+    X[7, 1] = np.nan
+    with pytest.raises(ValueError, match="NaN"):
+        KMeans(4, _fit=never, _seed=never).fit(X)
+
+
+@pytest.mark.gpu
+def test_gpu_estimator_float64_cloud_large_k(gpu):
+    """float64 D=3 cloud with K=4096 (beyond the dense engine's LDS stage): the
+    estimator routes it to the pruned engine (float32) and fits; labels equal the
+    oracle's canonical fit of the float32-cast centred cloud."""
+    from pcm_amd.estimator import KMeans
+    from oracle import lloyd_ref as R
+    rng = np.random.default_rng(5)
+    X = rng.random((60_000, 3)) * np.array([30.0, 1500.0, 2200.0])
+    init = X[np.sort(rng.choice(len(X), 4096, replace=False))]
+    km = KMeans(4096, init=init, n_init=1, max_iter=15, tol=0.0).fit(X)
+    Xc = X - X.mean(axis=0)
+    ref = R.lloyd_fit(Xc.astype(np.float32), (init - X.mean(axis=0)).astype(np.float32), max_iter=15, tol=0.0,
+                      fast=True)
+    np.testing.assert_array_equal(km.labels_, ref["labels"])
+    assert km.n_iter_ == ref["n_iter"] and km.cluster_centers_.dtype == np.float64
+
+
+@pytest.mark.gpu
+def test_gpu_dense_kmeanspp_rejects_nan(gpu):
+    import torch
+    from pcm_amd.dense import dense_kmeanspp
+    X = torch.rand(500, 6, dtype=torch.float64, device="cuda")
+    X[3, 2] = float("nan")
+    with pytest.raises(ValueError, match="NaN"):
+        dense_kmeanspp(X, 4, random_state=0)
