@@ -488,79 +488,50 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     e->sub = (e->d <= 3 && lloyd_slots(e) == LSLOT) ? 1 : 0;
     const int sh = e->sub ? e->d : 0;
     const long long nsub = nc << sh;
-    // Counting sort into key order (k_key_count, scan, k_key_scatter): 12 B/pt read twice
-    // + 16 B/pt written (xs + perm), vs a radix sort of (key, row) pairs and a random
-    // 12-B row gather.  PCM_LAYOUT_RADIX=1: the radix path (A/B measurement only).
-    static const bool radix = [] { const char *v = std::getenv("PCM_LAYOUT_RADIX"); return v && std::atoi(v) == 1; }();
-    size_t scan_bytes = 0;
-    if (rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
-                                (size_t)std::max(nc, nsub + 1), rocprim::plus<uint32_t>(), s) != hipSuccess)
-        return fail(PCM_E_HIP, "layout: rocprim size query failed");
-    size_t sort_bytes = 0;
+    // Key order: a radix sort of (key, row) pairs, then a 12-B row gather into
+    // AoSoA-4.  Counting sorts were measured slower at config 3 (100M points,
+    // 32768 keys): global-atomic counters 3.65 ms (count) + 7.35 ms (scatter), an
+    // LDS-privatised histogram 0.39 ms + 7.55 ms for its scatter (single-point
+    // writes into 32768 key ranges do not merge), vs 1.4 ms sort + 2.9 ms gather
+    // (DESIGN.md §3).
+    size_t sort_bytes = 0, scan_bytes = 0;
     unsigned bits = 1;
     while ((1LL << bits) < nsub) ++bits;
-    if (radix && rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                           (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)n, 0u, bits, s) != hipSuccess)
+    if (rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (uint32_t *)nullptr, (size_t)n, 0u, bits, s) != hipSuccess ||
+        rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)nc,
+                                rocprim::plus<uint32_t>(), s) != hipSuccess)
         return fail(PCM_E_HIP, "layout: rocprim size query failed");
-    const size_t o_cnt = 0, o_cur = align_up(o_cnt + (nsub + 1) * 4), o_tcnt = align_up(o_cur + (nsub + 1) * 4),
-                 o_keys = align_up(o_tcnt + nc * 4), o_keys2 = align_up(o_keys + (radix ? n * 4 : 0)),
-                 o_vals = align_up(o_keys2 + (radix ? n * 4 : 0)), o_tmp = align_up(o_vals + (radix ? n * 4 : 0)),
+    const size_t o_keys = 0, o_keys2 = align_up(o_keys + n * 4), o_vals = align_up(o_keys2 + n * 4),
+                 o_tcnt = align_up(o_vals + n * 4), o_tmp = align_up(o_tcnt + nc * 4),
                  ws_need = o_tmp + std::max(sort_bytes, scan_bytes);
     if (ensure(e->ws, e->cap_ws, ws_need) != hipSuccess) return fail(PCM_E_NOMEM, "layout scratch");
     char *wb = (char *)e->ws;
-    uint32_t *cnt = (uint32_t *)(wb + o_cnt), *cur = (uint32_t *)(wb + o_cur), *tcnt = (uint32_t *)(wb + o_tcnt),
-             *keys = (uint32_t *)(wb + o_keys), *keys2 = (uint32_t *)(wb + o_keys2), *vals = (uint32_t *)(wb + o_vals);
+    uint32_t *keys = (uint32_t *)(wb + o_keys), *keys2 = (uint32_t *)(wb + o_keys2), *vals = (uint32_t *)(wb + o_vals),
+             *tcnt = (uint32_t *)(wb + o_tcnt);
     void *tmp = wb + o_tmp;
 
-    int rc = 0;
-    if (!radix) {
-        HIPCHK(hipMemsetAsync(cnt, 0, (size_t)(nsub + 1) * 4, s));
-        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-            using TT = decltype(T);
-            constexpr int D = decltype(DD)::value;
-            k_key_count<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, cnt);
-            LAUNCHCHK();
-            return 0;
-        });
-        if (rc) return rc;
-        size_t sb = scan_bytes;
-        if (rocprim::exclusive_scan(tmp, sb, cnt, e->sub_start, 0u, (size_t)(nsub + 1), rocprim::plus<uint32_t>(), s) !=
-            hipSuccess)
-            return fail(PCM_E_HIP, "layout: key scan");
-        HIPCHK(hipMemcpyAsync(cur, e->sub_start, (size_t)nsub * 4, hipMemcpyDeviceToDevice, s));
-        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-            using TT = decltype(T);
-            constexpr int D = decltype(DD)::value;
-            k_key_scatter<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, cur, (TT *)e->xs, e->perm);
-            LAUNCHCHK();
-            k_xs_pad<TT, D><<<1, 64, 0, s>>>((TT *)e->xs, n, e->npad);
-            LAUNCHCHK();
-            return 0;
-        });
-        if (rc) return rc;
-    } else {
-        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-            using TT = decltype(T);
-            constexpr int D = decltype(DD)::value;
-            k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, keys, vals);
-            LAUNCHCHK();
-            return 0;
-        });
-        if (rc) return rc;
-        size_t tb = sort_bytes;
-        if (hipError_t err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))
-            return fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
-        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-            using TT = decltype(T);
-            constexpr int D = decltype(DD)::value;
-            k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs);
-            LAUNCHCHK();
-            return 0;
-        });
-        if (rc) return rc;
-        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nsub, e->sub_start);
+    int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, keys, vals);
         LAUNCHCHK();
-    }
+        return 0;
+    });
+    if (rc) return rc;
+    size_t tb = sort_bytes;
+    if (hipError_t err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))
+        return fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
+    rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs);
+        LAUNCHCHK();
+        return 0;
+    });
+    if (rc) return rc;
+    k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nsub, e->sub_start);
+    LAUNCHCHK();
     k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, sh, e->cell_start);
     LAUNCHCHK();
     k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap);

@@ -301,45 +301,6 @@ __global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long lo
     for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = src >= 0 ? X[src * D + a] : (T)0.0f;
 }
 
-// Counting sort of the layout (replaces a radix sort of (key, row) pairs + a
-// random row gather).  Pass 1: points per sort key (non-returning atomics).
-template <typename T, int D>
-__global__ __launch_bounds__(256) void k_key_count(const T *__restrict__ X, long long n, Grid g, int with_sub,
-                                                   uint32_t *__restrict__ counts) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    atomicAdd(counts + sort_key<T, D>(X, i, g, with_sub), 1u);
-}
-
-// Pass 2: every point claims the next slot of its key's range (cursor = the
-// exclusive scan of the counts) and is written there in AoSoA-4 order, with
-// perm[slot] = row.  Rows read sequentially; each key's slots fill one after the
-// other, so the writes merge in the caches instead of each costing an HBM burst.
-// The order inside a key depends on scheduling -- nothing downstream depends on
-// it (exact integer sums; labels are per point; relocation ties by global row).
-template <typename T, int D>
-__global__ __launch_bounds__(256) void k_key_scatter(const T *__restrict__ X, long long n, Grid g, int with_sub,
-                                                     uint32_t *__restrict__ cursor, T *__restrict__ xs,
-                                                     uint32_t *__restrict__ perm) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    T v[D];
-#pragma unroll
-    for (int a = 0; a < D; ++a) v[a] = X[i * D + a];
-    const uint32_t pos = atomicAdd(cursor + sort_key<T, D>(X, i, g, with_sub), 1u);
-#pragma unroll
-    for (int a = 0; a < D; ++a) xs[xs_index<D>(pos, a)] = v[a];
-    perm[pos] = (uint32_t)i;
-}
-
-// Zero the AoSoA padding slots [n, npad) (out-of-range lanes of the last groups).
-template <typename T, int D>
-__global__ void k_xs_pad(T *__restrict__ xs, long long n, long long npad) {
-    const long long i = n + threadIdx.x;
-    if (i < npad)
-        for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = (T)0.0f;
-}
-
 // cell_start[c] = first sorted index with key >= c, for c in [0, ncells]
 __global__ __launch_bounds__(256) void k_cell_starts(const uint32_t *__restrict__ keys, long long n, long long ncells,
                                                      uint32_t *__restrict__ start) {

@@ -197,9 +197,8 @@ def slab_proxy(args) -> dict:
     iters = args.warmup + args.steps
     X = synth_uniform(N, D, seed=0)
     C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0)
-    lo = X.min(0).values.double().cpu().numpy()
-    hi = X.max(0).values.double().cpu().numpy()
-    q = fixed_q(np.maximum(np.abs(lo), np.abs(hi)))
+    lo, hi, maxabs = Engine(D, K, torch.float32, max_iter=1).bbox(X)
+    q = fixed_q(maxabs)
     axis = int(np.argmax(hi - lo))
     inv = lloyd.SLAB_BINS / (hi[axis] - lo[axis])
     owner = lloyd.slab_owner(shard_hist(X, axis, lo[axis], inv, lloyd.SLAB_BINS).cpu().numpy(), P)

@@ -6,4 +6,4 @@ cd "$(dirname "$0")/.."
 mkdir -p tools/variants
 P=3d-point-cloud-multiday-imagery_amd
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I include "$@" \
-  -o tools/variants/lib_$name.so $P/csrc/pcm_engine.hip $P/csrc/pcm_dense.hip $P/csrc/pcm_stereo.hip
+  -o tools/variants/lib_$name.so $P/csrc/pcm_engine.hip $P/csrc/pcm_dense.hip $P/csrc/pcm_stereo.hip $P/csrc/pcm_shard.hip
