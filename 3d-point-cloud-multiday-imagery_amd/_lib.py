@@ -33,7 +33,7 @@ EXPORTS = [
     "pcm_dense_status", "pcm_dense_outputs", "pcm_dense_kmeanspp_workspace", "pcm_dense_kmeanspp",
     "pcm_photoconsistency", "pcm_lr_consistency",
     "pcm_layout_shard", "pcm_shard_hist", "pcm_shard_partition_workspace", "pcm_shard_partition",
-    "pcm_shard_scatter_labels", "pcm_assign_kernel_name",
+    "pcm_shard_scatter_labels", "pcm_assign_kernel_name", "pcm_layout_stream_bytes",
 ]
 ABI_VERSION = 3
 
@@ -122,6 +122,7 @@ def _declare(lib):
         "pcm_shard_partition": ([P, I, I64, I, I, D, D, I, P, I, I64, P, P, P, P, ctypes.c_size_t, P], I),
         "pcm_shard_scatter_labels": ([P, P, I64, I64, P, P], I),
         "pcm_assign_kernel_name": ([P, ctypes.c_char_p, ctypes.c_size_t], I),
+        "pcm_layout_stream_bytes": ([P, ctypes.POINTER(D), ctypes.POINTER(I64)], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

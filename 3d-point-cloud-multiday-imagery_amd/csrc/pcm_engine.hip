@@ -59,6 +59,11 @@ struct pcm_engine {
     uint32_t tile_cap = TILE;        // points per tile
     // device buffers (persistent: grown on demand, reused by later layouts, freed at destroy)
     void *xs = nullptr;
+    unsigned *xz = nullptr;          // compressed 8-B point records (fp32 D = 3, k_tile_compress)
+    uint4 *tmeta = nullptr;          // per-tile compression records
+    unsigned long long *zpts = nullptr;   // points in compressed tiles (device counter)
+    bool use_xz = false;             // the current layout has a compressed stream
+    size_t cap_xz = 0, cap_tmeta = 0;
     uint32_t *perm = nullptr;
     void *lab = nullptr;             // sorted-order labels: uint16 when k <= 65535, else int32
     uint32_t *cell_start = nullptr;
@@ -157,11 +162,12 @@ void free_layout(pcm_engine *e) {
 
 void free_buffers(pcm_engine *e) {
     void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->ws,
-                  e->sub_start};
+                  e->sub_start, e->xz, e->tmeta};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
     e->tile_off = nullptr; e->ws = nullptr; e->sub_start = nullptr; e->cap_sub = 0;
+    e->xz = nullptr; e->tmeta = nullptr; e->cap_xz = e->cap_tmeta = 0; e->use_xz = false;
     e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
     e->cap_xs = e->cap_lab = e->cap_perm = e->cap_cells = e->cap_fc = e->cap_tiles = e->cap_ws = 0;
     free_layout(e);
@@ -330,6 +336,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->cand_stats, 3 * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->empty_idx, (size_t)k * sizeof(int));
     err = err ? err : hipMalloc(&e->ntiles_dev, 2 * sizeof(uint32_t));
+    err = err ? err : hipMalloc(&e->zpts, sizeof(unsigned long long));
     err = err ? err : hipMemset(e->partials, 0, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMemset(e->ctrl, 0, sizeof(Ctrl));
     if (err != hipSuccess) {
@@ -352,7 +359,7 @@ int pcm_engine_destroy(pcm_engine *e) {
     free_buffers(e);
     void *ps[] = {e->C, e->Cn, e->cref, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
                   e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx, e->ntiles_dev,
-                  e->grows};
+                  e->grows, e->zpts};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -543,6 +550,17 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     LAUNCHCHK();
     k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles, e->tile_cap);
     LAUNCHCHK();
+    // compressed point stream for k_lloyd1 (fp32, D = 3; PCM_XZ=0 disables it: A/B measurement only)
+    static const bool xz_on = [] { const char *v = std::getenv("PCM_XZ"); return !(v && std::atoi(v) == 0); }();
+    e->use_xz = xz_on && e->dtype == PCM_F32 && e->d == 3;
+    HIPCHK(hipMemsetAsync(e->zpts, 0, sizeof(unsigned long long), s));
+    if (e->use_xz) {
+        HIPCHK(ensure(e->xz, e->cap_xz, (size_t)e->npad * 8));
+        HIPCHK(ensure(e->tmeta, e->cap_tmeta, (size_t)e->ntiles_cap * sizeof(uint4)));
+        k_tile_compress<<<(int)e->ntiles_cap, 256, 0, s>>>((const float *)e->xs, e->tiles, e->ntiles_dev, e->tmeta,
+                                                           e->xz, e->zpts);
+        LAUNCHCHK();
+    }
     // stream-ordered: no host synchronisation (work queued later on `stream`
     // sees the layout; X must not be modified by other streams meanwhile)
     e->layout_ready = true;
@@ -632,6 +650,8 @@ static int lloyd_slots(const pcm_engine *e) {
 static LloydArgs lloyd_args(pcm_engine *e) {
     LloydArgs A{};
     A.xs = e->xs;
+    A.xz = e->use_xz ? e->xz : nullptr;
+    A.tmeta = e->use_xz ? e->tmeta : nullptr;
     A.npad = e->npad;
     A.tiles = e->tiles;
     A.ntiles = e->ntiles_dev;
@@ -1012,6 +1032,17 @@ int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid) 
     }
     *ntiles = e->ntiles;
     for (int a = 0; a < MAXD; ++a) grid[a] = e->g.G[a];
+    return 0;
+}
+
+int pcm_layout_stream_bytes(pcm_engine *e, double *bytes, int64_t *compressed_points) {
+    if (!e || !bytes || !compressed_points) return fail(PCM_E_ARG, "bad argument");
+    if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
+    unsigned long long z = 0;
+    HIPCHK(hipMemcpy(&z, e->zpts, sizeof(z), hipMemcpyDeviceToHost));
+    const double raw = (double)e->d * (double)tsize(e->dtype);
+    *compressed_points = (int64_t)z;
+    *bytes = (double)z * 8.0 + (double)(e->n - (long long)z) * raw;
     return 0;
 }
 

@@ -352,6 +352,83 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
     }
 }
 
+// Compressed point stream (fp32, D = 3).  Inside one tile (one cell, <= TILE
+// points) each axis spans a short range, so every coordinate's fp32 bit pattern
+// is the tile's minimum pattern on that axis plus a small unsigned delta (the
+// patterns of same-signed floats are ordered by magnitude).  When every axis is
+// single-signed over the tile and the three delta widths sum to <= 64 bits, the
+// tile's points are stored as 8-byte records d0 | d1 << w0 | d2 << (w0 + w1) in
+// `xz` (AoSoA-4: [lo0 lo1 lo2 lo3][hi0 hi1 hi2 hi3] per group of 4 points, at
+// byte 8 * position); k_lloyd1 then streams 8 instead of 12 bytes per point and
+// rebuilds the EXACT fp32 values (lossless: labels and sums are unchanged).
+// tmeta[t] = {min0, min1, min2, 1 << 31 | w0 | w1 << 8 | w2 << 16}, or .w = 0
+// (raw tile: 12-B AoSoA-4 `xs`).  Uniform [0,1)^3 cloud with 32^3 cells: cells
+// with an axis index >= 1 need <= 23 + 21 + 20 bits; ~91 % of the points.
+__device__ __forceinline__ unsigned zwidth(unsigned span) { return span ? 32u - (unsigned)__clz(span) : 0u; }
+
+__global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__ xs, const uint4 *__restrict__ tiles,
+                                                       const uint32_t *__restrict__ ntiles, uint4 *__restrict__ tmeta,
+                                                       unsigned *__restrict__ xz, unsigned long long *__restrict__ zpts) {
+    const unsigned t = blockIdx.x;
+    if (t >= *ntiles) return;
+    const uint4 tr = tiles[t];
+    const unsigned start = tr.y, end = tr.z;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    unsigned mn[3] = {~0u, ~0u, ~0u}, mx[3] = {0u, 0u, 0u}, sor[3] = {0u, 0u, 0u}, sand[3] = {1u, 1u, 1u};
+    for (unsigned i = start + tid; i < end; i += 256) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const unsigned b = __float_as_uint(xs[xs_index<3>(i, a)]);
+            mn[a] = min(mn[a], b);
+            mx[a] = max(mx[a], b);
+            sor[a] |= b >> 31;
+            sand[a] &= b >> 31;
+        }
+    }
+    __shared__ unsigned smn[4][3], smx[4][3], sso[4][3], ssa[4][3];
+    __shared__ uint4 meta;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        for (int o = 32; o > 0; o >>= 1) {
+            mn[a] = min(mn[a], (unsigned)__shfl_xor((int)mn[a], o));
+            mx[a] = max(mx[a], (unsigned)__shfl_xor((int)mx[a], o));
+            sor[a] |= (unsigned)__shfl_xor((int)sor[a], o);
+            sand[a] &= (unsigned)__shfl_xor((int)sand[a], o);
+        }
+        if (lane == 0) { smn[wv][a] = mn[a]; smx[wv][a] = mx[a]; sso[wv][a] = sor[a]; ssa[wv][a] = sand[a]; }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned w[3], lo[3], total = 0;
+        bool ok = true;
+        for (int a = 0; a < 3; ++a) {
+            unsigned m0 = ~0u, m1 = 0u, so = 0u, sa = 1u;
+            for (int k = 0; k < 4; ++k) { m0 = min(m0, smn[k][a]); m1 = max(m1, smx[k][a]); so |= sso[k][a]; sa &= ssa[k][a]; }
+            lo[a] = m0;
+            w[a] = zwidth(m1 - m0);
+            ok = ok && (so == sa) && w[a] <= 31u;
+            total += w[a];
+        }
+        ok = ok && total <= 64u;
+        meta = make_uint4(lo[0], lo[1], lo[2], ok ? (0x80000000u | w[0] | (w[1] << 8) | (w[2] << 16)) : 0u);
+        tmeta[t] = meta;
+        if (ok) atomicAdd(zpts, (unsigned long long)(end - start));
+    }
+    __syncthreads();
+    const uint4 m = meta;
+    if (!(m.w >> 31)) return;
+    const unsigned w0 = m.w & 0xffu, w1 = (m.w >> 8) & 0xffu;
+    for (unsigned i = start + tid; i < end; i += 256) {
+        const unsigned long long d0 = __float_as_uint(xs[xs_index<3>(i, 0)]) - m.x;
+        const unsigned long long d1 = __float_as_uint(xs[xs_index<3>(i, 1)]) - m.y;
+        const unsigned long long d2 = __float_as_uint(xs[xs_index<3>(i, 2)]) - m.z;
+        const unsigned long long v = d0 | (d1 << w0) | (d2 << (w0 + w1));
+        const size_t g = (size_t)(i >> 2) * 8u + (i & 3u);
+        xz[g] = (unsigned)v;
+        xz[g + 4] = (unsigned)(v >> 32);
+    }
+}
+
 // ------------------------------------------------------------------ candidates
 // Candidate lists of every fine cell, in one launch, without global-memory
 // round trips inside the per-cell work.  Block (I, b) owns coarse cell I
@@ -896,6 +973,31 @@ __device__ __forceinline__ void load_x(Raw<T, D> &r, rsrc_t rs, unsigned off_pt)
     }
 }
 #define LOAD_X(dst, off) load_x<T, D>(dst, rx, off)
+// fp32 D = 3 with compressed tiles: the same three b128 loads per item whatever the
+// tile's format (identical vmcnt bookkeeping on every path): raw tiles read
+// x/y/z words at 12 B per point; compressed tiles read lo/hi words at 8 B per
+// point from rA and send the third load out of range (zeros, no traffic).
+__device__ __forceinline__ void load_xa(Raw<float, 3> &r, rsrc_t rA, rsrc_t rx, unsigned off_pt, unsigned bpp, bool zc) {
+    const unsigned boff = off_pt * bpp;
+    const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rA, boff, 0, PCM_XLOAD_CPOL);
+    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rA, boff + 16u, 0, PCM_XLOAD_CPOL);
+    const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rx, zc ? 0xFFFFFFF0u : boff + 32u, 0, PCM_XLOAD_CPOL);
+    r.w[0] = v0[0]; r.w[1] = v0[1]; r.w[2] = v0[2]; r.w[3] = v0[3];
+    r.w[4] = v1[0]; r.w[5] = v1[1]; r.w[6] = v1[2]; r.w[7] = v1[3];
+    r.w[8] = v2[0]; r.w[9] = v2[1]; r.w[10] = v2[2]; r.w[11] = v2[3];
+}
+// exact fp32 coordinates of a compressed item (k_tile_compress): base + delta bits
+__device__ __forceinline__ void unpack_z(const Raw<float, 3> &r, float (&x)[4][3], const uint4 &zm, unsigned sh1,
+                                         unsigned sh2, unsigned m0, unsigned m1, unsigned m2) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const unsigned lo = r.w[e], hi = r.w[4 + e];
+        const unsigned long long v = ((unsigned long long)hi << 32) | lo;
+        x[e][0] = __uint_as_float(zm.x + (lo & m0));
+        x[e][1] = __uint_as_float(zm.y + ((unsigned)(v >> sh1) & m1));
+        x[e][2] = __uint_as_float(zm.z + ((unsigned)(v >> sh2) & m2));
+    }
+}
 // AoSoA-4 (xs_index): word a*4 + e holds coordinate a of the lane's point e
 template <int D>
 __device__ __forceinline__ void unpack_x(const Raw<float, D> &r, float (&x)[4][D]) {
@@ -954,6 +1056,8 @@ template <int D, int LS = LSLOT> struct AccL {
 
 struct LloydArgs {
     const void *xs;                 // packed AoS [npad][D] of T, cell order
+    const unsigned *xz;             // compressed 8-B records (fp32 D = 3 tiles with tmeta .w bit 31), or null
+    const uint4 *tmeta;             // per-tile compression record (k_tile_compress), or null
     long long npad;
     const uint4 *tiles;             // {cell, start, end, -}
     const uint32_t *fc_cnt;         // candidate count per cell (FULL: all K)
@@ -1401,7 +1505,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     uint4 tr = tiles[t];
     unsigned nt = *A.ntiles;
     unsigned gate = A.ctrl->halt | A.ctrl->done;
+    constexpr bool ZOK = sizeof(T) == 4 && D == 3;   // compressed tiles exist only for fp32 D = 3
+    uint4 zm = make_uint4(0u, 0u, 0u, 0u);
+    if (ZOK && A.tmeta) zm = A.tmeta[t];
     asm volatile("" : "+s"(tr.x), "+s"(tr.y), "+s"(tr.z), "+s"(nt), "+s"(gate));   // keep the loads above the exits
+    asm volatile("" : "+s"(zm.x), "+s"(zm.y), "+s"(zm.z), "+s"(zm.w));
     if (gate != 0u || t >= nt) return;
     DBG_L(0);
     const unsigned cell = tr.x, start = tr.y, end = tr.z;
@@ -1419,14 +1527,25 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     const unsigned base0 = start & ~3u;
     const int nr = (int)((end - base0 + 4 * TPB - 1) / (4 * TPB));
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
+    // compressed tile (k_tile_compress): 8-B records from xz, decoded exactly
+    const bool zc = ZOK && (zm.w >> 31);
+    const unsigned zw0 = zm.w & 0xffu, zw1 = (zm.w >> 8) & 0xffu, zw2 = (zm.w >> 16) & 0xffu;
+    const unsigned zsh1 = zw0, zsh2 = zw0 + zw1;
+    const unsigned zm0 = (1u << zw0) - 1u, zm1 = (1u << zw1) - 1u, zm2 = (1u << zw2) - 1u;
+    const unsigned bpp = zc ? 8u : (unsigned)(D * sizeof(T));
+    const rsrc_t rA = make_rsrc(zc ? (const void *)A.xz : A.xs, (unsigned long long)A.npad * bpp);
     // lanes past the tile's end get the out-of-range offset: zeros, no memory traffic
     auto item_off = [&](int rr) -> unsigned {
         const unsigned o = base0 + (unsigned)rr * 4u * TPB + 4u * tid;
         return (rr < nr && o < end) ? o : 0x0ffffff0u;
     };
+    auto ldx = [&](Raw<T, D> &dst, unsigned off) {
+        if constexpr (ZOK) load_xa(dst, rA, rx, off, bpp, zc);
+        else load_x<T, D>(dst, rx, off);
+    };
     Raw<T, D> xa, xb, xc;
-    LOAD_X(xa, item_off(0));
-    LOAD_X(xb, item_off(1));
+    ldx(xa, item_off(0));
+    ldx(xb, item_off(1));
     for (int e = tid; e < AccL<D, LS>::words; e += TPB) acc[e] = 0u;
     if (kOvf)
         for (int e = tid; e < (CAPF - LS) * (D + 1); e += TPB) ovf[e] = 0ull;
@@ -1533,7 +1652,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     constexpr int VM = 2 * NL;
     constexpr int WAIT_PREV = 0x0F70 | (VM & 0xF) | ((VM >> 4) << 14);   // vmcnt(VM) expcnt(7) lgkmcnt(15)
     auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx, int r) {
-        LOAD_X(nx, item_off(r + 2));
+        ldx(nx, item_off(r + 2));
         if (r >= nr) {
             // padding step (nr not a multiple of 3): no compute, but the same
             // wait as a computing step, so that every path reaches the loop
@@ -1545,7 +1664,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         const unsigned rbase = base0 + (unsigned)r * 4u * TPB;
         const unsigned i0 = rbase + 4u * tid;
         float x[4][D];
-        unpack_x<D>(cx, x);
+        if constexpr (ZOK) {
+            if (zc) unpack_z(cx, x, zm, zsh1, zsh2, zm0, zm1, zm2);
+            else unpack_x<D>(cx, x);
+        } else {
+            unpack_x<D>(cx, x);
+        }
         int bj[4];
 #ifdef PCM_ABL_NOSCAN
         if (true) {

@@ -186,6 +186,12 @@ class Engine:
         _lib.check(self.lib.pcm_layout_info(self.h, ctypes.byref(nc), ctypes.byref(nt), g), "pcm_layout_info")
         return dict(ncells=nc.value, ntiles=nt.value, grid=list(g)[: self.d])
 
+    def stream_bytes(self) -> dict:
+        """Bytes the assign kernel streams per iteration (compressed tiles at 8 B/pt)."""
+        b, z = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(self.lib.pcm_layout_stream_bytes(self.h, ctypes.byref(b), ctypes.byref(z)), "pcm_layout_stream_bytes")
+        return dict(bytes=b.value, compressed_points=z.value)
+
     def assign_kernel(self) -> str:
         buf = ctypes.create_string_buffer(128)
         _lib.check(self.lib.pcm_assign_kernel_name(self.h, buf, 128), "pcm_assign_kernel_name")

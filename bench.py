@@ -359,7 +359,7 @@ def main():
     init_rows = np.sort(np.random.default_rng(1).choice(N, K, replace=False))
     C0 = synth_rows(init_rows, D, seed=0)
     total_iters = args.warmup + args.steps
-    max_iter = total_iters + 16
+    max_iter = 2 * total_iters + 16      # timed steps + the eager event pass of as many
     group = None
     eng = Engine(D, K, torch.float32, max_iter=max_iter)
     torch.cuda.synchronize()
@@ -431,7 +431,7 @@ def main():
         # eager pass of the same kernels right after the timed graph replay (and, at
         # N > 1, where events inside the timed region would cost ~15 % of a shard's step)
         eng.timing(True)
-        iterate(4)
+        iterate(args.steps)
         tm = eng.timing_read()
         timing = "HIP events on an eager pass of the same kernels right after the timed graph replay"
     else:
@@ -482,7 +482,13 @@ def main():
         else:
             workload = (f"Lloyd K-means iteration, N={N} K={K} D={D} fp32 (config 4, {world} GPUs, "
                         f"{'spatial slabs' if args.shard == 'slab' else 'row shards'}, all-reduce every iteration)")
-        # the iteration kernel streams only the points (labels are recomputed, not stored)
+        # the iteration kernel streams only the points (labels are recomputed, not stored):
+        # 8 B/pt in compressed tiles (exact fp32 rebuilt from per-tile bases + delta bits),
+        # D*4 B/pt elsewhere -- the roofline uses those streamed bytes, measured per layout
+        # (roofline basis: SURVEY.md §8d's algorithmic bytes = one D*4-byte row per point per
+        # iteration; the stream actually moved is reported beside it and by the PMC traffic)
+        sb = eng.stream_bytes()
+        stream_bytes = sb["bytes"]
         bytes_pt = D * 4
         achieved = bytes_pt * n_local / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0
         traffic, traffic_src = pmc_traffic(N, K, D, world)
@@ -513,6 +519,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": eng.assign_kernel(),
                          "algorithmic_bytes_per_point": bytes_pt,
+                         "stream_bytes_per_launch": stream_bytes, "compressed_points": sb["compressed_points"],
+                         "stream_GBps": stream_bytes / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0,
                          "avg_launch_ms": assign_ms, "timing": timing + ("" if world == 1 else " (max over ranks)")},
             "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"]},
             "candidates": cand,

@@ -158,6 +158,10 @@ int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream);
 
 /* Layout facts for diagnostics: cells, tiles, grid dims (host ints). */
 int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid /*[4]*/);
+/* Bytes the assign kernel streams per iteration for the current layout (points
+ * in compressed tiles at 8 B, the others at d * sizeof(dtype)) and the number
+ * of compressed points (synchronising; see DESIGN.md §3, compressed stream). */
+int pcm_layout_stream_bytes(pcm_engine *e, double *bytes, int64_t *compressed_points);
 /* Name of the assign-kernel variant the current layout launches per iteration
  * (e.g. "k_lloyd1<float,3,8,false>"), for measurement records. */
 int pcm_assign_kernel_name(pcm_engine *e, char *buf, size_t n);
