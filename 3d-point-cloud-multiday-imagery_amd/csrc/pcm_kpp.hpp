@@ -118,9 +118,37 @@ __device__ __forceinline__ long long kpp_cube_cell(const Grid &g, const int (&i0
     return encode(f, g.G, D);
 }
 
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+// Inclusive wave scan of a u64 by DPP moves of both halves (row_shr 1/2/4/8
+// inside rows of 16, then row_bcast 15 / 31 across rows; out-of-row sources
+// read 0): VALU-only, no LDS crossbar round trips -- the ds_bpermute chains of
+// 64-bit shuffles cost ~7 us of k_kpp_search's 33 (tools/kpp_timing.py).
+// The whole wave must be active.
+__device__ __forceinline__ unsigned long long wave_scan_u64(unsigned long long v) {
+#define PCM_DPP_ADD(ctrl, rmask)                                                                              \
+    {                                                                                                         \
+        const unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)v, ctrl, rmask, 0xF, false);          \
+        const unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), ctrl, rmask, 0xF, false);  \
+        v += ((unsigned long long)hi << 32) | lo;                                                             \
+    }
+    PCM_DPP_ADD(0x111, 0xF)
+    PCM_DPP_ADD(0x112, 0xF)
+    PCM_DPP_ADD(0x114, 0xF)
+    PCM_DPP_ADD(0x118, 0xF)
+    PCM_DPP_ADD(0x142, 0xA)
+    PCM_DPP_ADD(0x143, 0xC)
+#undef PCM_DPP_ADD
     return v;
+}
+
+// lane 63 of the inclusive scan, broadcast (uniform)
+__device__ __forceinline__ unsigned long long wave_last_u64(unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    return wave_last_u64(wave_scan_u64(v));
 }
 
 __device__ __forceinline__ float wave_max_f(float v) {
@@ -193,11 +221,7 @@ __global__ __launch_bounds__(256) void k_kpp_init(const float *__restrict__ xs, 
 // prefix of this thread.
 __device__ __forceinline__ unsigned long long kpp_block_exscan(unsigned long long v, unsigned long long *wtot) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    unsigned long long inc = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long u = __shfl_up(inc, o);
-        if (lane >= o) inc += u;
-    }
+    const unsigned long long inc = wave_scan_u64(v);
     if (lane == 63) wtot[wv] = inc;
     __syncthreads();
     unsigned long long base = 0ull;
@@ -279,27 +303,25 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
     if (mine) {   // wave-uniform
         // the chunk holding the target from the chunk totals (register chunks:
         // static indices), then one wave prefix scan of that chunk
-        unsigned long long r = base, x = 0ull;
+        unsigned long long r = base, x = 0ull, xi = 0ull;
         int uc = -1;
 #pragma unroll
         for (int u = 0; u < CU; ++u) {
-            const unsigned long long ct = wave_sum_u64(v[u]);
-            if (uc < 0 && u < nch && (r + ct >= tg)) { uc = u; x = v[u]; }
+            const unsigned long long inc = wave_scan_u64(v[u]);   // independent scans: VALU ILP
+            const unsigned long long ct = wave_last_u64(inc);
+            if (uc < 0 && u < nch && (r + ct >= tg)) { uc = u; x = v[u]; xi = inc; }
             if (uc < 0) r += ct;
         }
         for (int u = CU; uc < 0 && u < nch; ++u) {   // past the register cache (n > ~134M points)
             const long long b = sb + 64LL * u + lane;
             const unsigned long long y = b < se ? bsum[b] : 0ull;
-            const unsigned long long ct = wave_sum_u64(y);
-            if (r + ct >= tg) { uc = u; x = y; } else { r += ct; }
+            const unsigned long long inc = wave_scan_u64(y);
+            const unsigned long long ct = wave_last_u64(inc);
+            if (r + ct >= tg) { uc = u; x = y; xi = inc; } else { r += ct; }
         }
         if (uc >= 0) {
             const long long b = sb + 64LL * uc + lane;
-            unsigned long long inc = x;
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned long long y = __shfl_up(inc, o);
-                if (lane >= o) inc += y;
-            }
+            const unsigned long long inc = xi;
             const unsigned long long ex = r + inc - x;
             if (b < se && r + inc >= tg && (b == 0 || ex < tg)) {   // first block whose inclusive prefix reaches tg
                 s_blk = b;
