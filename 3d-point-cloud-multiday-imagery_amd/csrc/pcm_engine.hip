@@ -1290,6 +1290,10 @@ int pcm_debug_timing(unsigned long long *out, int nblocks) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_t), (size_t)nblocks * 16 * sizeof(unsigned long long)));
     return 0;
 }
+int pcm_debug_timing_eval(unsigned long long *out, int nblocks) {
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_e), (size_t)nblocks * 8 * sizeof(unsigned long long)));
+    return 0;
+}
 int pcm_debug_timing_lloyd(unsigned long long *out, int nblocks) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_l), (size_t)nblocks * 4 * sizeof(unsigned long long)));
     return 0;

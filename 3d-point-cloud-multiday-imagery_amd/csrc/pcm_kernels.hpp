@@ -460,7 +460,12 @@ __device__ unsigned long long g_dbg_t[8192][16];
 #define DBG_V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = (unsigned long long)(v); } while (0)
 __device__ unsigned long long g_dbg_l[65536][4];
 #define DBG_L(k) do { if (threadIdx.x == 0 && blockIdx.x < 65536) g_dbg_l[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ unsigned long long g_dbg_e[8192][8];
+#define DBG_E(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_e[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define DBG_EV(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_e[blockIdx.x][k] = (unsigned long long)(v); } while (0)
 #else
+#define DBG_E(k) do { } while (0)
+#define DBG_EV(k, v) do { } while (0)
 #define DBG_T(k) do { } while (0)
 #define DBG_V(k, v) do { } while (0)
 #define DBG_L(k) do { } while (0)

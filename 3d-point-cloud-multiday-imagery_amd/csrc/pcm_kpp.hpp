@@ -388,6 +388,7 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
     __shared__ long long s_off[KPP_LMAX + 1];
     __shared__ float4 s_cand[KPP_LMAX];
     const int tid = threadIdx.x, lane = tid & 63;
+    DBG_E(0);
     const float gmax = __uint_as_float(ctl->gmax_acc[c & 1]);
     if (tid < L) {
         const float4 cd = ctl->cand[tid];
@@ -406,8 +407,11 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
     }
     __syncthreads();
     const long long total = s_off[L];
+    DBG_E(1);
+    DBG_EV(5, total);
     const long long wid = (blockIdx.x * (long long)blockDim.x + tid) >> 6;
     const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    unsigned dbg_cells = 0;
     unsigned long long dw[KPP_LMAX];
 #pragma unroll
     for (int q = 0; q < KPP_LMAX; ++q) dw[q] = 0ull;
@@ -468,6 +472,7 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
                 reach = kpp_reaches<D>(g, cell, s_cand[l], cm);
             }
             unsigned long long bits = __ballot(reach);
+            dbg_cells += (unsigned)__popcll(bits);
             while (bits) {
                 const int src = __builtin_ctzll(bits);
                 bits &= bits - 1ull;
@@ -485,6 +490,9 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
             }
         }
     }
+    DBG_E(2);
+    DBG_EV(4, dbg_cells);
+    (void)dbg_cells;
     // waves that reached no cell hold zeros: skip their L wave reductions (in the
     // late steps most of the grid's waves have no item, and 8 x 12 cross-lane
     // moves per idle wave were a large share of the launch)

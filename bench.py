@@ -300,6 +300,9 @@ def main():
                     help="1-GPU proxy of config 4 at P GPUs: the P slab engines of lloyd.prepare's split run on this "
                          "GPU, their statistics summed between the kernels (the all-reduce, emulated); per-rank "
                          "k_lloyd1 + k_step times from HIP events (the per-rank iteration cost, RCCL excluded)")
+    ap.add_argument("--clustered", type=int, default=0, metavar="C",
+                    help="degenerate-cloud check: C tight Gaussian clusters (sigma 0.004) + 1%% uniform background "
+                         "instead of the uniform cloud (pruning stress: FULL candidate lists, long lists)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher test: each rank prints its RANK/WORLD_SIZE as JSON and exits before any GPU call")
     args = ap.parse_args()
@@ -358,6 +361,16 @@ def main():
     X = synth_uniform(hi_row - lo_row, D, seed=0, start=lo_row)
     init_rows = np.sort(np.random.default_rng(1).choice(N, K, replace=False))
     C0 = synth_rows(init_rows, D, seed=0)
+    if args.clustered > 0:
+        # C tight clusters: each row's cluster and offset from the counter-based uniforms
+        # (torch elementwise plumbing on the device), 1 % of the rows stay uniform background
+        g = torch.Generator(device="cuda").manual_seed(5)
+        centres = torch.rand((args.clustered, D), generator=g, device="cuda")
+        cid = (X[:, 0] * args.clustered).long().clamp_(0, args.clustered - 1)
+        noise = torch.randn(X.shape, generator=g, device="cuda") * 0.004
+        keep = (X[:, 1] < 0.01).unsqueeze(1)
+        X = torch.where(keep, X, centres[cid] + noise).contiguous()
+        C0 = X[torch.as_tensor(init_rows - lo_row if world == 1 else init_rows % X.shape[0], device="cuda")].contiguous()
     total_iters = args.warmup + args.steps
     max_iter = 2 * total_iters + 16      # timed steps + the eager event pass of as many
     group = None
@@ -507,7 +520,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic: counter-based U[0,1)^3 cloud generated on device (splitmix64), init = rows "
                     "sorted(default_rng(1).choice(N, K))",
-            "config": {"workload": workload,
+            "config": {"workload": workload + (f"; CLUSTERED cloud ({args.clustered} clusters), not config 3"
+                                                if args.clustered else ""),
                        "n_points": N, "k": K, "d": D,
                        "parallelism": f"dp{world} ({'spatial slabs' if args.shard == 'slab' else 'row shards'})"
                                       if world > 1 else "single GPU",

@@ -16,3 +16,9 @@ python tools/pmc_summary.py k_lloyd $T/pmc_FETCH_SIZE $T/pmc_WRITE_SIZE > $T/pmc
 bash tools/prof.sh $T/prof --steps 20 --warmup 3 --fit | tail -14 || exit 1
 PCM_PMC_JSON=$T/pmc_k_lloyd.json timeout -k 10 400 python bench.py --fit --cloud --stereo > $T/bench.txt 2>&1 || { tail -20 $T/bench.txt; exit 1; }
 tail -1 $T/bench.txt
+for P in 2 4 8; do
+  timeout -k 10 200 python bench.py --slab-of $P --steps 20 --warmup 3 > $T/proxy$P.json 2>&1 || { tail -20 $T/proxy$P.json; exit 1; }
+  tail -1 $T/proxy$P.json | cut -c1-400
+done
+timeout -k 10 200 python bench.py --gpus 2 --backend gloo --n 20000000 --no-cpu --fit-iters 0 --steps 5 --warmup 2 > $T/gloo2.txt 2>&1 || { tail -20 $T/gloo2.txt; exit 1; }
+tail -1 $T/gloo2.txt | cut -c1-300

@@ -27,3 +27,15 @@ for b in range(L):
 g = t[L:L + 64]
 print("gmax blocks: start p50 %.2f max %.2f  end p50 %.2f max %.2f" % (us(np.median(g[:, 0] - t0)), us((g[:, 0] - t0).max()),
                                                                    us(np.median(g[:, 8] - t0)), us((g[:, 8] - t0).max())))
+# last k_kpp_eval launch (c = k - 1): per-block phase stamps (DBG_E) and reached cells of wave 0
+lib.pcm_debug_timing_eval.argtypes = [ctypes.c_void_p, ctypes.c_int]
+ev = np.zeros((8192, 8), np.uint64)
+assert lib.pcm_debug_timing_eval(ev.ctypes.data_as(ctypes.c_void_p), 8192) == 0
+e = ev.astype(np.int64)
+nb = int((e[:, 0] > 0).sum())
+e = e[:nb]
+t0 = e[:, 0].min()
+print(f"eval blocks {nb}: items total {int(e[0, 5])}; reached cells of wave 0 p50 {np.median(e[:, 4]):.0f} max {e[:, 4].max()}")
+for k, name in ((0, "start"), (1, "setup"), (2, "cells done")):
+    v = (e[:, k] - t0) / 100.0
+    print(f"  {name:10s} us after first start: p50 {np.median(v):6.2f} p90 {np.percentile(v, 90):6.2f} max {v.max():6.2f}")
