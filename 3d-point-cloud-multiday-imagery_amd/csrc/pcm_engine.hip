@@ -64,6 +64,14 @@ struct pcm_engine {
     unsigned long long *zpts = nullptr;   // points in compressed tiles (device counter)
     bool use_xz = false;             // the current layout has a compressed stream
     size_t cap_xz = 0, cap_tmeta = 0;
+    // crowded layouts (tight clusters): Morton levels of the in-cell order and the tile lists
+    int zlev = 0;
+    float4 *tbox = nullptr;          // [tile][2] exact point box
+    uint32_t *tl_cnt = nullptr;      // [tile] list length (tiles of FULL cells) or FULL
+    float4 *tl_rec = nullptr;        // [tile][CAPF]
+    int32_t *tl_lab = nullptr;       // [tile][CAPF]
+    uint32_t *zcnt = nullptr;        // occupancy sample counts [ncells + 1]
+    size_t cap_tbox = 0, cap_tlc = 0, cap_tlr = 0, cap_tll = 0, cap_zcnt = 0;
     uint32_t *perm = nullptr;
     void *lab = nullptr;             // sorted-order labels: uint16 when k <= 65535, else int32
     uint32_t *cell_start = nullptr;
@@ -162,12 +170,14 @@ void free_layout(pcm_engine *e) {
 
 void free_buffers(pcm_engine *e) {
     void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->ws,
-                  e->sub_start, e->xz, e->tmeta};
+                  e->sub_start, e->xz, e->tmeta, e->tbox, e->tl_cnt, e->tl_rec, e->tl_lab, e->zcnt};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
     e->tile_off = nullptr; e->ws = nullptr; e->sub_start = nullptr; e->cap_sub = 0;
     e->xz = nullptr; e->tmeta = nullptr; e->cap_xz = e->cap_tmeta = 0; e->use_xz = false;
+    e->tbox = nullptr; e->tl_cnt = nullptr; e->tl_rec = nullptr; e->tl_lab = nullptr; e->zcnt = nullptr;
+    e->cap_tbox = e->cap_tlc = e->cap_tlr = e->cap_tll = e->cap_zcnt = 0; e->zlev = 0;
     e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
     e->cap_xs = e->cap_lab = e->cap_perm = e->cap_cells = e->cap_fc = e->cap_tiles = e->cap_ws = 0;
     free_layout(e);
@@ -425,6 +435,54 @@ int pcm_layout_shard(pcm_engine *e, const uint32_t *rows, int64_t n_global, void
     return 0;
 }
 
+static unsigned cell_bits(long long nc) {
+    unsigned b = 0;
+    while ((1LL << b) < nc) ++b;
+    return b;
+}
+
+// Crowded-cell detection (tile lists, k_tile_cand): the cell counts of a strided
+// sample of up to 2^22 points, scaled to n.  A cell expected to hold more than
+// ZCROWD tiles' worth of points gets its points ordered by zlev Morton levels,
+// enough that a level-zlev box of the fullest cell holds ~1/8 tile (the lists
+// are only needed when K exceeds CAPF).  One host read-back of 4 bytes.
+// PCM_ZLEV forces the level count (tests: crowded order on small clouds).
+static int choose_zlev(pcm_engine *e, const void *X, hipStream_t s) {
+    e->zlev = 0;
+    const long long n = e->n, nc = e->g.ncells;
+    const int d = e->d;
+    const unsigned cb = cell_bits(nc);
+    const int zmax = std::min(6, (int)((32 - (int)cb) / d));
+    if (const char *v = std::getenv("PCM_ZLEV")) {
+        e->zlev = std::max(0, std::min(zmax, std::atoi(v)));
+        return 0;
+    }
+    constexpr double ZCROWD = 4.0;
+    if (!e->g.prune || e->k <= CAPF || n < (long long)(ZCROWD * e->tile_cap) || zmax < 1) return 0;
+    const long long m = std::min(n, 1LL << 22), stride = n / m;
+    HIPCHK(ensure(e->zcnt, e->cap_zcnt, (size_t)(nc + 1) * sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(e->zcnt, 0, (size_t)(nc + 1) * sizeof(uint32_t), s));
+    int rc = dispatch_td(e->dtype, d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        k_zsample<TT, D><<<blocks_for(m), 256, 0, s>>>((const TT *)X, m, stride, e->g, e->zcnt);
+        LAUNCHCHK();
+        return 0;
+    });
+    if (rc) return rc;
+    k_umax<<<(int)std::min<long long>(1024, std::max(1LL, (nc + 255) / 256)), 256, 0, s>>>(e->zcnt, nc, e->zcnt + nc);
+    LAUNCHCHK();
+    uint32_t mx = 0;
+    HIPCHK(hipMemcpyAsync(&mx, e->zcnt + nc, sizeof(mx), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double est = (double)mx * (double)n / (double)m;
+    if (est <= ZCROWD * e->tile_cap) return 0;
+    int z = 1;
+    while (z < zmax && std::ldexp(1.0, d * z) < 8.0 * est / e->tile_cap) ++z;
+    e->zlev = z;
+    return 0;
+}
+
 int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gidx0, void *stream) {
     if (!e || !q) return fail(PCM_E_ARG, "bad argument");
     if (!e->have_bbox) return fail(PCM_E_STATE, "pcm_layout_bbox must run first");
@@ -493,6 +551,8 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     // coarse grids whose k_lloyd1 variant uses sub-cell masks (the 16-slot D <= 3
     // one, see lloyd_slots); else the cell id
     e->sub = (e->d <= 3 && lloyd_slots(e) == LSLOT) ? 1 : 0;
+    if (int rc = choose_zlev(e, X, s)) return rc;
+    if (e->zlev > 0) e->sub = 0;
     const int sh = e->sub ? e->d : 0;
     const long long nsub = nc << sh;
     // Key order: a radix sort of (key, row) pairs, then a 12-B row gather into
@@ -504,6 +564,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     size_t sort_bytes = 0, scan_bytes = 0;
     unsigned bits = 1;
     while ((1LL << bits) < nsub) ++bits;
+    if (e->zlev > 0) bits = cell_bits(nc) + (unsigned)(e->d * e->zlev);   // <= 32 (choose_zlev)
     if (rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                   (uint32_t *)nullptr, (size_t)n, 0u, bits, s) != hipSuccess ||
         rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)nc,
@@ -521,7 +582,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
-        k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, keys, vals);
+        k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, e->zlev, keys, vals);
         LAUNCHCHK();
         return 0;
     });
@@ -537,9 +598,13 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         return 0;
     });
     if (rc) return rc;
-    k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nsub, e->sub_start);
-    LAUNCHCHK();
-    k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, sh, e->cell_start);
+    if (e->zlev > 0) {   // Morton-ordered cells: cell starts straight from the keys' cell bits
+        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, e->cell_start, e->d * e->zlev);
+    } else {
+        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nsub, e->sub_start);
+        LAUNCHCHK();
+        k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, sh, e->cell_start);
+    }
     LAUNCHCHK();
     k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap);
     LAUNCHCHK();
@@ -561,8 +626,23 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
                                                            e->xz, e->zpts);
         LAUNCHCHK();
     }
+    if (e->zlev > 0) {   // crowded layout: exact tile boxes and tile-list storage
+        HIPCHK(ensure(e->tbox, e->cap_tbox, (size_t)e->ntiles_cap * 2 * sizeof(float4)));
+        HIPCHK(ensure(e->tl_cnt, e->cap_tlc, (size_t)e->ntiles_cap * sizeof(uint32_t)));
+        HIPCHK(ensure(e->tl_rec, e->cap_tlr, (size_t)e->ntiles_cap * CAPF * sizeof(float4)));
+        HIPCHK(ensure(e->tl_lab, e->cap_tll, (size_t)e->ntiles_cap * CAPF * sizeof(int32_t)));
+        rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+            using TT = decltype(T);
+            constexpr int D = decltype(DD)::value;
+            k_tile_box<TT, D><<<(int)e->ntiles_cap, 256, 0, s>>>((const TT *)e->xs, e->tiles, e->ntiles_dev, e->tbox);
+            LAUNCHCHK();
+            return 0;
+        });
+        if (rc) return rc;
+    }
     // stream-ordered: no host synchronisation (work queued later on `stream`
-    // sees the layout; X must not be modified by other streams meanwhile)
+    // sees the layout; X must not be modified by other streams meanwhile),
+    // except choose_zlev's occupancy read-back
     e->layout_ready = true;
     return 0;
 }
@@ -622,6 +702,19 @@ static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     });
 }
 
+// Tile lists of the crowded cells at the current centres (before every assign
+// launch of a crowded layout; gate: skip when the fit has halted or finished).
+static int launch_tile_lists(pcm_engine *e, hipStream_t s, int gate) {
+    if (e->zlev <= 0 || e->n == 0) return 0;
+    return dispatch_d(e->d, [&](auto DD) -> int {
+        constexpr int D = decltype(DD)::value;
+        k_tile_cand<D><<<(int)e->ntiles_cap, 256, 0, s>>>(e->tiles, e->ntiles_dev, e->fc_cnt, e->tbox, e->C, e->k,
+                                                          e->tl_cnt, e->tl_rec, e->tl_lab, e->ctrl, gate);
+        LAUNCHCHK();
+        return 0;
+    });
+}
+
 // Persistent grid: as many 256-thread blocks as are co-resident (occupancy
 // query), never more blocks than tiles.
 static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
@@ -667,6 +760,9 @@ static LloydArgs lloyd_args(pcm_engine *e) {
     A.sub_start = e->sub_start;
     A.sub = e->sub;
     A.g = e->g;
+    A.tl_cnt = e->zlev > 0 ? e->tl_cnt : nullptr;
+    A.tl_rec = e->zlev > 0 ? e->tl_rec : nullptr;
+    A.tl_lab = e->zlev > 0 ? e->tl_lab : nullptr;
     return A;
 }
 
@@ -675,6 +771,7 @@ static LloydArgs lloyd_args(pcm_engine *e) {
 // into inert[0..3].  Not gated.
 static int launch_labels(pcm_engine *e, hipStream_t s, unsigned long long *inert) {
     if (int rc = launch_candidates(e, s, 0)) return rc;
+    if (int rc = launch_tile_lists(e, s, 0)) return rc;
     LloydArgs A = lloyd_args(e);
     return dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
@@ -730,6 +827,7 @@ static int timing_mark(pcm_engine *e, int which, hipStream_t s) {
 // otherwise into the single-GPU parity half partials[iter & 1].
 static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
     if (int rc = timing_mark(e, 0, s)) return rc;
+    if (int rc = launch_tile_lists(e, s, 1)) return rc;   // crowded layouts only
     if (int rc = timing_mark(e, 1, s)) return rc;
     LloydArgs A = lloyd_args(e);
     if (to_stats) {
@@ -1070,6 +1168,27 @@ int pcm_candidate_stats(pcm_engine *e, double *mean, int *mx, int64_t *full_cell
     *mean = nonfull > 0 ? (double)h[0] / (double)nonfull : 0.0;
     *mx = (int)h[1];
     *full_cells = (int64_t)h[2];
+    return 0;
+}
+
+int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *full_tiles, int64_t *listed_tiles, int64_t *listed_len,
+                        void *stream) {
+    if (!e || !zlev || !full_tiles || !listed_tiles || !listed_len) return fail(PCM_E_ARG, "bad argument");
+    if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
+    *zlev = e->zlev;
+    *full_tiles = *listed_tiles = *listed_len = 0;
+    if (e->zlev <= 0 || e->n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(e->cand_stats, 0, 3 * sizeof(unsigned long long), s));
+    k_tile_list_stats<<<blocks_for(e->ntiles_cap), 256, 0, s>>>(e->tiles, e->ntiles_dev, e->fc_cnt, e->tl_cnt,
+                                                                 e->cand_stats);
+    LAUNCHCHK();
+    unsigned long long h[3];
+    HIPCHK(hipMemcpyAsync(h, e->cand_stats, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *full_tiles = (int64_t)h[0];
+    *listed_tiles = (int64_t)h[1];
+    *listed_len = (int64_t)h[2];
     return 0;
 }
 

@@ -246,28 +246,44 @@ __global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long lo
 // within a cell the points of one sub-cell are contiguous.  The half test uses
 // the same fp64 cell coordinate as the binning (clamped cells: a point on the
 // top face lands in the upper half); sub-cell boxes carry the binning margin on
-// both sides of the split (k_lloyd1).
+// both sides of the split (k_lloyd1).  Crowded layouts (zlev > 0) instead append
+// a Morton code of zlev bisections of the cell (level 1 = the sub-cell bits,
+// then the next finer halves, axis 0 first within a level), so the tiles of a
+// crowded cell are compact boxes (tile lists, k_tile_cand).
 template <typename T, int D>
-__device__ __forceinline__ uint32_t sort_key(const T *__restrict__ X, long long i, const Grid &g, int with_sub) {
+__device__ __forceinline__ uint32_t sort_key(const T *__restrict__ X, long long i, const Grid &g, int with_sub,
+                                             int zlev) {
     int idx[MAXD];
-    uint32_t sub = 0;
+    uint32_t sub = 0, fz[MAXD];
 #pragma unroll
     for (int a = 0; a < D; ++a) {
         double t = ((double)to_f<T>(X[i * D + a]) - g.lo[a]) * g.inv[a];
         int v = (int)floor(t);
         v = v < 0 ? 0 : (v >= g.G[a] ? g.G[a] - 1 : v);
         idx[a] = v;
-        sub = (sub << 1) | ((t - (double)v >= 0.5) ? 1u : 0u);
+        const double fr = t - (double)v;
+        sub = (sub << 1) | ((fr >= 0.5) ? 1u : 0u);
+        const int top = (1 << zlev) - 1;
+        int m = (int)floor(fr * (double)(1 << zlev));
+        fz[a] = (uint32_t)(m < 0 ? 0 : (m > top ? top : m));
     }
-    return with_sub ? ((uint32_t)encode(idx, g.G, D) << D) | sub : (uint32_t)encode(idx, g.G, D);
+    const uint32_t cell = (uint32_t)encode(idx, g.G, D);
+    if (zlev > 0) {
+        uint32_t z = 0;
+        for (int l = zlev - 1; l >= 0; --l)
+#pragma unroll
+            for (int a = 0; a < D; ++a) z = (z << 1) | ((fz[a] >> l) & 1u);
+        return (cell << (D * zlev)) | z;
+    }
+    return with_sub ? (cell << D) | sub : cell;
 }
 
 template <typename T, int D>
 __global__ __launch_bounds__(256) void k_subcellid(const T *__restrict__ X, long long n, Grid g, int with_sub,
-                                                   uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+                                                   int zlev, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    keys[i] = sort_key<T, D>(X, i, g, with_sub);
+    keys[i] = sort_key<T, D>(X, i, g, with_sub, zlev);
     vals[i] = (uint32_t)i;
 }
 
@@ -302,12 +318,13 @@ __global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long lo
 }
 
 // cell_start[c] = first sorted index with key >= c, for c in [0, ncells]
+// (keys >> shift: the cell ids of Morton-ordered crowded layouts)
 __global__ __launch_bounds__(256) void k_cell_starts(const uint32_t *__restrict__ keys, long long n, long long ncells,
-                                                     uint32_t *__restrict__ start) {
+                                                     uint32_t *__restrict__ start, int shift = 0) {
     long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i > n) return;
-    long long prev = (i == 0) ? -1 : (long long)keys[i - 1];
-    long long cur = (i == n) ? ncells : (long long)keys[i];
+    long long prev = (i == 0) ? -1 : (long long)(keys[i - 1] >> shift);
+    long long cur = (i == n) ? ncells : (long long)(keys[i] >> shift);
     for (long long c = prev + 1; c <= cur; ++c) start[c] = (uint32_t)i;
 }
 
@@ -426,6 +443,168 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
         const size_t g = (size_t)(i >> 2) * 8u + (i & 3u);
         xz[g] = (unsigned)v;
         xz[g + 4] = (unsigned)(v >> 32);
+    }
+}
+
+// ------------------------------------------------------------------ crowded cells: tile lists
+// A uniform grid cannot follow tight clusters: a cell that holds a whole
+// cluster holds its hundreds of centres too, its list overflows CAPF (FULL) and
+// every point of it scans all K (a 16-cluster K = 4096 cloud: 20 ms per
+// iteration, VALU-bound).  When the layout finds crowded cells (an occupancy
+// sample, pcm_layout_build) it orders each cell's points by a Morton code of
+// `zlev` further bisections (sort_key), so a tile -- a run of <= TILE points of
+// one cell -- covers a compact piece of the cell; k_tile_box records each
+// tile's exact point box, and before every assign launch k_tile_cand builds,
+// for the tiles of FULL cells, a list over that box with the same exact
+// dominance test as the cell lists (any box holding the points is valid).
+
+// Occupancy sample: counts[cell of point i * stride] += 1, i < m; counts[ncells]
+// := the largest count afterwards (k_umax).
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_zsample(const T *__restrict__ X, long long m, long long stride, Grid g,
+                                                 uint32_t *__restrict__ counts) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const long long p = i * stride;
+    int idx[MAXD];
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        const double t = ((double)to_f<T>(X[p * D + a]) - g.lo[a]) * g.inv[a];
+        int v = (int)floor(t);
+        idx[a] = v < 0 ? 0 : (v >= g.G[a] ? g.G[a] - 1 : v);
+    }
+    atomicAdd(counts + encode(idx, g.G, D), 1u);
+}
+
+__global__ __launch_bounds__(256) void k_umax(const uint32_t *__restrict__ v, long long n, uint32_t *__restrict__ out) {
+    uint32_t m = 0;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        m = max(m, v[i]);
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+// Exact fp32 box of every tile's points: tbox[2t] = lower, tbox[2t + 1] = upper corner.
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_tile_box(const T *__restrict__ xs, const uint4 *__restrict__ tiles,
+                                                  const uint32_t *__restrict__ ntiles, float4 *__restrict__ tbox) {
+    const unsigned t = blockIdx.x;
+    if (t >= *ntiles) return;
+    const uint4 tr = tiles[t];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    float mn[D], mx[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) { mn[a] = __builtin_inff(); mx[a] = -__builtin_inff(); }
+    for (unsigned i = tr.y + tid; i < tr.z; i += 256)
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const float v = to_f<T>(xs[xs_index<D>(i, a)]);
+            mn[a] = fminf(mn[a], v);
+            mx[a] = fmaxf(mx[a], v);
+        }
+    __shared__ float smn[4][MAXD], smx[4][MAXD];
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        for (int o = 32; o > 0; o >>= 1) {
+            mn[a] = fminf(mn[a], __shfl_xor(mn[a], o));
+            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o));
+        }
+        if (lane == 0) { smn[wv][a] = mn[a]; smx[wv][a] = mx[a]; }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float lo[4] = {0.f, 0.f, 0.f, 0.f}, hi[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int a = 0; a < D; ++a) {
+            lo[a] = fminf(fminf(smn[0][a], smn[1][a]), fminf(smn[2][a], smn[3][a]));
+            hi[a] = fmaxf(fmaxf(smx[0][a], smx[1][a]), fmaxf(smx[2][a], smx[3][a]));
+        }
+        tbox[2 * (size_t)t] = make_float4(lo[0], lo[1], lo[2], lo[3]);
+        tbox[2 * (size_t)t + 1] = make_float4(hi[0], hi[1], hi[2], hi[3]);
+    }
+}
+
+// List of one tile of a FULL cell over its point box, at the current centres:
+// reference r = a centre of least max distance to the box, then every centre
+// not provably dominated by r (prunable), compacted in ascending centroid index
+// (the strict-'<' scan keeps the lowest index on ties).  tl_cnt[t] = the length,
+// or FULL past CAPF (the tile scans all K).  Tiles of other cells are skipped
+// (k_lloyd1 reads tl_cnt only for FULL cells).
+template <int D>
+__global__ __launch_bounds__(256) void k_tile_cand(const uint4 *__restrict__ tiles, const uint32_t *__restrict__ ntiles,
+                                                   const uint32_t *__restrict__ fc_cnt, const float4 *__restrict__ tbox,
+                                                   const float4 *__restrict__ C, int K, uint32_t *__restrict__ tl_cnt,
+                                                   float4 *__restrict__ tl_rec, int32_t *__restrict__ tl_lab,
+                                                   const Ctrl *__restrict__ ctrl, int gate) {
+    const unsigned t = blockIdx.x;
+    if (gate && gated(ctrl)) return;
+    if (t >= *ntiles) return;
+    const uint4 tr = tiles[t];
+    if (fc_cnt[tr.x] != FULL) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const float4 lo4 = tbox[2 * (size_t)t], hi4 = tbox[2 * (size_t)t + 1];
+    double blo[MAXD], bhi[MAXD];
+#pragma unroll
+    for (int a = 0; a < D; ++a) { blo[a] = (double)comp(lo4, a); bhi[a] = (double)comp(hi4, a); }
+    double best = __builtin_inf();
+    int bj = 0;
+    for (int j = tid; j < K; j += 256) {
+        const double md = maxdist<D>(blo, bhi, C[j]);
+        if (md < best) { best = md; bj = j; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const int oj = __shfl_xor(bj, o);
+        if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+    }
+    __shared__ double s_b[4];
+    __shared__ int s_j[4];
+    __shared__ unsigned s_w[4];
+    if (lane == 0) { s_b[wv] = best; s_j[wv] = bj; }
+    __syncthreads();
+    int rj = s_j[0];
+    double rb = s_b[0];
+    for (int w = 1; w < 4; ++w)
+        if (s_b[w] < rb || (s_b[w] == rb && s_j[w] < rj)) { rb = s_b[w]; rj = s_j[w]; }
+    const float4 r = C[rj];
+    unsigned base = 0;
+    for (int j0 = 0; j0 < K; j0 += 256) {
+        const int j = j0 + tid;
+        const bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r);
+        const unsigned long long bal = __ballot(keep);
+        if (lane == 0) s_w[wv] = (unsigned)__popcll(bal);
+        __syncthreads();
+        unsigned off = base, total = 0;
+        for (int w = 0; w < 4; ++w) {
+            off += (w < wv) ? s_w[w] : 0u;
+            total += s_w[w];
+        }
+        const unsigned pos = off + (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
+        if (keep && pos < (unsigned)CAPF) {
+            tl_rec[(size_t)t * CAPF + pos] = C[j];
+            tl_lab[(size_t)t * CAPF + pos] = j;
+        }
+        base += total;
+        __syncthreads();   // s_w is rewritten by the next chunk
+        if (base > (unsigned)CAPF) break;   // block-uniform
+    }
+    if (tid == 0) tl_cnt[t] = base <= (unsigned)CAPF ? base : FULL;
+}
+
+// Tile-list summary: out[0] += tiles of FULL cells, out[1] += those with a
+// tile list, out[2] += the lengths of those lists.
+__global__ __launch_bounds__(256) void k_tile_list_stats(const uint4 *__restrict__ tiles,
+                                                         const uint32_t *__restrict__ ntiles,
+                                                         const uint32_t *__restrict__ fc_cnt,
+                                                         const uint32_t *__restrict__ tl_cnt,
+                                                         unsigned long long *__restrict__ out) {
+    const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (t >= *ntiles) return;
+    if (fc_cnt[tiles[t].x] != FULL) return;
+    atomicAdd(out, 1ull);
+    const uint32_t c = tl_cnt[t];
+    if (c != FULL) {
+        atomicAdd(out + 1, 1ull);
+        atomicAdd(out + 2, (unsigned long long)c);
     }
 }
 
@@ -1078,6 +1257,9 @@ struct LloydArgs {
     const uint32_t *sub_start;      // [(ncells << D) + 1] sub-cell starts (k_lloyd1's per-round candidate masks)
     int sub;                        // the layout is sorted by sub-cell (else sub_start is [ncells + 1])
     Grid g;
+    const uint32_t *tl_cnt;         // crowded layouts: per-tile list length for tiles of FULL cells (or FULL), else null
+    const float4 *tl_rec;           // [tile][CAPF] records of the tile lists (k_tile_cand)
+    const int32_t *tl_lab;
 };
 
 struct TileL {
@@ -1149,11 +1331,18 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned 
     for (unsigned t = blockIdx.x; t < nt; t += G) {
         uint4 tr = A.tiles[t];
         tr.w = A.fc_cnt[tr.x];
+        const float4 *trec = lrec + (size_t)tr.x * CAPF;
+        const int32_t *tlab = llab + (size_t)tr.x * CAPF;
+        if (tr.w == FULL && A.tl_cnt && A.tl_cnt[t] != FULL) {   // crowded cell: the tile's own list
+            tr.w = A.tl_cnt[t];
+            trec = A.tl_rec + (size_t)t * CAPF;
+            tlab = A.tl_lab + (size_t)t * CAPF;
+        }
         const TileL h = make_tile(tr, A.K);
         __syncthreads();
         if (!h.full && tid < h.mm) {
-            crec[tid] = lrec[(size_t)h.cell * CAPF + tid];
-            cid[tid] = llab[(size_t)h.cell * CAPF + tid];
+            crec[tid] = trec[tid];
+            cid[tid] = tlab[tid];
         }
         __syncthreads();
         Raw<T, D> cur, nxt;
@@ -1214,7 +1403,25 @@ __device__ __forceinline__ void scan4_s(const float4 *__restrict__ C, int mm, co
         const float4 c = C[0];
         for (int e = 0; e < 4; ++e) { bd[e] = dist_canon<D>(x[e], c); bj[e] = 0; }
     }
-    for (int j = 1; j < mm; ++j) {
+    // Groups of 8 centres are fetched before any is used, so eight scalar
+    // loads share one latency instead of paying it per centre (FULL tiles
+    // scan all K; measured 20 ms/iter on a 16-cluster K=4096 cloud before).
+    int j = 1;
+    for (; j + 8 <= mm; j += 8) {
+        float4 cg[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cg[u] = C[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            for (int e = 0; e < 4; ++e) {
+                float dd = dist_canon<D>(x[e], cg[u]);
+                bool lt = dd < bd[e];
+                bd[e] = lt ? dd : bd[e];
+                bj[e] = lt ? j + u : bj[e];
+            }
+        }
+    }
+    for (; j < mm; ++j) {
         const float4 c = C[j];
         for (int e = 0; e < 4; ++e) {
             float dd = dist_canon<D>(x[e], c);
@@ -1524,7 +1731,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         r0 = fc_rec[(size_t)cell * CAPF + tid];
         l0 = fc_lab[(size_t)cell * CAPF + tid];
     }
-    const uint32_t cnt = fc_cnt[cell];
+    uint32_t cnt = fc_cnt[cell];
+    // crowded cell (FULL list): the tile's own list when k_tile_cand built one
+    const float4 *lrec = fc_rec + (size_t)cell * CAPF;
+    const int32_t *llab = fc_lab + (size_t)cell * CAPF;
+    bool tl = false;
+    if (cnt == FULL && A.tl_cnt) {
+        const uint32_t tc = A.tl_cnt[t];
+        if (tc != FULL) {
+            cnt = tc;
+            lrec = A.tl_rec + (size_t)t * CAPF;
+            llab = A.tl_lab + (size_t)t * CAPF;
+            tl = true;
+        }
+    }
     constexpr int NSUB = 1 << D;
     uint32_t ss[NSUB + 1];   // the cell's sub-cell starts (uniform: scalar loads)
 #pragma unroll
@@ -1560,12 +1780,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         if (tid < LS) cid[tid] = tid;
     } else {
         if (tid < LSPEC && tid < mm) {
-            crec[tid] = r0;
-            cid[tid] = l0;
+            crec[tid] = tl ? lrec[tid] : r0;
+            cid[tid] = tl ? llab[tid] : l0;
         }
         for (int j = LSPEC + tid; j < mm; j += TPB) {   // long lists (rare at D <= 3)
-            crec[j] = fc_rec[(size_t)cell * CAPF + j];
-            cid[j] = fc_lab[(size_t)cell * CAPF + j];
+            crec[j] = lrec[j];
+            cid[j] = llab[j];
         }
     }
     uint32_t *const myacc = acc + (tid & (AW - 1));
@@ -1587,7 +1807,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     // 12.5M shard: 47.8 -> 43.5 us per launch); at config 3 (lists of ~2.7)
     // and D = 4 (16 sub-cells) the mask phase at the block's start cost more
     // than the shorter scans saved (217 -> 225 us, 415 -> 488 us)
-    const bool use_mask = MASK && A.sub && !full && mm >= MASK_MIN && A.g.prune;
+    const bool use_mask = MASK && A.sub && !full && !tl && mm >= MASK_MIN && A.g.prune;
     if (use_mask) {
         int ci[MAXD];
         for (int a = D - 1, c = (int)cell; a >= 0; --a) {   // cell ids fit 32 bits (sort keys)

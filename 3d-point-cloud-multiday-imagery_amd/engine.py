@@ -16,6 +16,9 @@ from . import _lib
 
 PCM_F32, PCM_F16 = 0, 1
 RELOC_RECORD_BYTES = 32
+# one engine holds fewer than 2^28 - 16 padded points (pcm_engine.hip, pcm_layout_build's check);
+# larger clouds are sharded over engines / ranks
+ENGINE_MAX_POINTS = (1 << 28) - 4096
 
 
 def _stream():
@@ -201,7 +204,14 @@ class Engine:
         mean, mx, full = ctypes.c_double(), ctypes.c_int(), ctypes.c_int64()
         _lib.check(self.lib.pcm_candidate_stats(self.h, ctypes.byref(mean), ctypes.byref(mx), ctypes.byref(full),
                                                 _stream()), "pcm_candidate_stats")
-        return dict(mean=mean.value, max=mx.value, full_cells=full.value)
+        out = dict(mean=mean.value, max=mx.value, full_cells=full.value)
+        z, ft, lt, ll = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(self.lib.pcm_tile_list_stats(self.h, ctypes.byref(z), ctypes.byref(ft), ctypes.byref(lt),
+                                                ctypes.byref(ll), _stream()), "pcm_tile_list_stats")
+        if z.value > 0:   # crowded layout: tiles of FULL cells and their own lists
+            out.update(zlev=z.value, full_tiles=ft.value, listed_tiles=lt.value,
+                       tile_list_mean=(ll.value / lt.value) if lt.value else 0.0)
+        return out
 
 
 def _dtype_code(X: torch.Tensor) -> int:

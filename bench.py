@@ -189,15 +189,16 @@ def slab_proxy(args) -> dict:
     import torch
 
     from pcm_amd import lloyd
-    from pcm_amd.engine import Engine, shard_hist, shard_partition, synth_rows, synth_uniform
+    from pcm_amd.engine import ENGINE_MAX_POINTS, Engine, shard_hist, shard_partition, synth_rows, synth_uniform
     from pcm_amd.fixed import fixed_q
 
     torch.cuda.set_device(0)
     N, K, D, P = args.n, args.k, args.d, args.slab_of
     iters = args.warmup + args.steps
-    X = synth_uniform(N, D, seed=0)
-    C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0)
-    lo, hi, maxabs = Engine(D, K, torch.float32, max_iter=1).bbox(X)
+    pdt = torch.float16 if args.dtype == "f16" else torch.float32
+    X = synth_uniform(N, D, seed=0).to(pdt)
+    C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0).to(pdt).float()
+    lo, hi, maxabs = Engine(D, K, pdt, max_iter=1).bbox(X)
     q = fixed_q(maxabs)
     axis = int(np.argmax(hi - lo))
     inv = lloyd.SLAB_BINS / (hi[axis] - lo[axis])
@@ -207,7 +208,7 @@ def slab_proxy(args) -> dict:
     for r in range(P):
         Xr, rr = Xp[off:off + int(cnt[r])], rows[off:off + int(cnt[r])]
         off += int(cnt[r])
-        e = Engine(D, K, torch.float32, max_iter=iters + 4)
+        e = Engine(D, K, pdt, max_iter=iters + 4)
         e.bbox(Xr)
         e.set_shard(rr, N)
         e.build(Xr, q, 0)
@@ -254,20 +255,25 @@ def slab_proxy(args) -> dict:
     ok = all(np.array_equal(C_slab, e.centers().cpu().numpy()) for e in engines)
     info = [dict(e.layout_info(), points=int(e.n), kernel=e.assign_kernel(), **e.candidate_stats()) for e in engines]
     del engines
-    one = Engine(D, K, torch.float32, max_iter=iters + 4)
-    lloyd.prepare(one, X, lloyd.LOCAL)
-    one.begin(C0, 0.0, iters + 4)
-    one.iterate(iters)
-    bitwise = ok and np.array_equal(C_slab, one.centers().cpu().numpy())
+    if N <= ENGINE_MAX_POINTS:
+        one = Engine(D, K, pdt, max_iter=iters + 4)
+        lloyd.prepare(one, X, lloyd.LOCAL)
+        one.begin(C0, 0.0, iters + 4)
+        one.iterate(iters)
+        bitwise = bool(ok and np.array_equal(C_slab, one.centers().cpu().numpy()))
+    else:       # one engine cannot hold the whole cloud: the P slab engines agreeing is the check left
+        bitwise = None
     a_ms, s_ms = t_assign / args.steps, t_step / args.steps
     per_rank = (a_ms + s_ms) * 1e3
     return {"metric": "per-rank Lloyd iteration cost at P GPUs (1-GPU slab proxy, all-reduce excluded)",
             "value": float(per_rank.max()), "unit": "us/iter (max over ranks)", "higher_is_better": False,
             "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "slab_of": P,
-            "config": {"workload": f"config 4 split {P} ways: N={N} K={K} D={D} fp32, slabs of axis {axis}"},
+            "config": {"workload": f"{'config 5' if args.dtype == 'f16' else 'config 4'} split {P} ways: N={N} "
+                                   f"K={K} D={D} {args.dtype}, slabs of axis {axis}"},
             "per_rank_us": {"assign": (a_ms * 1e3).round(2).tolist(), "step": (s_ms * 1e3).round(2).tolist(),
                             "total": per_rank.round(2).tolist()},
-            "slabs": info, "centres_bitwise_equal_single_engine": bool(bitwise)}
+            "slabs": info, "centres_bitwise_equal_single_engine": bitwise,
+            "slab_engines_agree": bool(ok)}
 
 
 def main():
@@ -300,6 +306,8 @@ def main():
                     help="1-GPU proxy of config 4 at P GPUs: the P slab engines of lloyd.prepare's split run on this "
                          "GPU, their statistics summed between the kernels (the all-reduce, emulated); per-rank "
                          "k_lloyd1 + k_step times from HIP events (the per-rank iteration cost, RCCL excluded)")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f16"],
+                    help="point dtype (f16: config 5's storage; the arithmetic stays canonical fp32)")
     ap.add_argument("--clustered", type=int, default=0, metavar="C",
                     help="degenerate-cloud check: C tight Gaussian clusters (sigma 0.004) + 1%% uniform background "
                          "instead of the uniform cloud (pruning stress: FULL candidate lists, long lists)")
@@ -358,6 +366,7 @@ def main():
     N, K, D = args.n, args.k, args.d
     lo_row = N * rank // world
     hi_row = N * (rank + 1) // world
+    pdt = torch.float16 if args.dtype == "f16" else torch.float32
     X = synth_uniform(hi_row - lo_row, D, seed=0, start=lo_row)
     init_rows = np.sort(np.random.default_rng(1).choice(N, K, replace=False))
     C0 = synth_rows(init_rows, D, seed=0)
@@ -371,10 +380,13 @@ def main():
         keep = (X[:, 1] < 0.01).unsqueeze(1)
         X = torch.where(keep, X, centres[cid] + noise).contiguous()
         C0 = X[torch.as_tensor(init_rows - lo_row if world == 1 else init_rows % X.shape[0], device="cuda")].contiguous()
+    if pdt == torch.float16:      # config 5 storage: the points and the initial centres rounded to fp16
+        X = X.to(pdt).contiguous()
+        C0 = C0.to(pdt).float()
     total_iters = args.warmup + args.steps
     max_iter = 2 * total_iters + 16      # timed steps + the eager event pass of as many
     group = None
-    eng = Engine(D, K, torch.float32, max_iter=max_iter)
+    eng = Engine(D, K, pdt, max_iter=max_iter)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -469,7 +481,7 @@ def main():
         # row order): a fresh engine (device buffers allocated) and the same
         # engine fitting again (persistent buffers reused)
         fit = {"iters": args.fit_iters}
-        eng2 = Engine(D, K, torch.float32, max_iter=args.fit_iters)
+        eng2 = Engine(D, K, pdt, max_iter=args.fit_iters)
         for key in ("cold_ms", "warm_ms"):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -490,11 +502,12 @@ def main():
 
     if rank == 0:
         n_local = int(eng.n)      # points this rank's engine holds (its slab at N > 1)
-        if world == 1:
-            workload = f"Lloyd K-means iteration, N={N} K={K} D={D} fp32 (config 3, 1 GPU)"
-        else:
-            workload = (f"Lloyd K-means iteration, N={N} K={K} D={D} fp32 (config 4, {world} GPUs, "
-                        f"{'spatial slabs' if args.shard == 'slab' else 'row shards'}, all-reduce every iteration)")
+        shape = (N, K, D, args.dtype)
+        named = {(100_000_000, 1024, 3, "f32"): "config 3" if world == 1 else "config 4",
+                 (500_000_000, 4096, 4, "f16"): "config 5", (1_000_000, 64, 3, "f32"): "config 2"}.get(shape)
+        where = "1 GPU" if world == 1 else (f"{world} GPUs, {'spatial slabs' if args.shard == 'slab' else 'row shards'}, "
+                                            f"all-reduce every iteration")
+        workload = f"Lloyd K-means iteration, N={N} K={K} D={D} {args.dtype} ({(named + ', ') if named else ''}{where})"
         # the iteration kernel streams only the points (labels are recomputed, not stored):
         # 8 B/pt in compressed tiles (exact fp32 rebuilt from per-tile bases + delta bits),
         # D*4 B/pt elsewhere -- the roofline uses those streamed bytes, measured per layout
@@ -502,7 +515,7 @@ def main():
         # iteration; the stream actually moved is reported beside it and by the PMC traffic)
         sb = eng.stream_bytes()
         stream_bytes = sb["bytes"]
-        bytes_pt = D * 4
+        bytes_pt = D * (2 if pdt == torch.float16 else 4)
         achieved = bytes_pt * n_local / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0
         traffic, traffic_src = pmc_traffic(N, K, D, world)
         value = N * args.steps / dt
@@ -517,7 +530,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": args.dtype,
             "data": "synthetic: counter-based U[0,1)^3 cloud generated on device (splitmix64), init = rows "
                     "sorted(default_rng(1).choice(N, K))",
             "config": {"workload": workload + (f"; CLUSTERED cloud ({args.clustered} clusters), not config 3"
@@ -536,7 +549,8 @@ def main():
                          "stream_bytes_per_launch": stream_bytes, "compressed_points": sb["compressed_points"],
                          "stream_GBps": stream_bytes / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0,
                          "avg_launch_ms": assign_ms, "timing": timing + ("" if world == 1 else " (max over ranks)")},
-            "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"]},
+            "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"],
+                                      "tile_lists": tm.get("candidates_ms", 0.0)},
             "candidates": cand,
             "layout_ms": layout_ms,
         }
@@ -553,7 +567,7 @@ def main():
         if kpp_ms is not None:
             out["kmeanspp_ms"] = kpp_ms   # GPU k-means++ seeding of the same cloud (K centres), host prep included
         if not args.no_cpu and world == 1:
-            out["cpu_baseline"] = cpu_baseline(X.cpu().numpy(), C0.cpu().numpy())
+            out["cpu_baseline"] = cpu_baseline(X.float().cpu().numpy(), C0.cpu().numpy())
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

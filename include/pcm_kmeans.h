@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PCM_ABI_VERSION 3
+#define PCM_ABI_VERSION 4
 
 enum pcm_dtype { PCM_F32 = 0, PCM_F16 = 1, PCM_F64 = 2 /* dense path only */ };
 
@@ -167,6 +167,12 @@ int pcm_layout_stream_bytes(pcm_engine *e, double *bytes, int64_t *compressed_po
 int pcm_assign_kernel_name(pcm_engine *e, char *buf, size_t n);
 /* Mean/max fine candidate-list length of the last iteration (synchronising). */
 int pcm_candidate_stats(pcm_engine *e, double *mean, int *max, int64_t *full_cells, void *stream);
+/* Crowded layouts (cells holding many tiles' worth of points, e.g. tight
+ * clusters): the Morton levels of the in-cell point order (0: not crowded),
+ * the tiles of FULL cells at the last iteration, how many of them got a tile
+ * list and those lists' summed length (synchronising). */
+int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *full_tiles, int64_t *listed_tiles, int64_t *listed_len,
+                        void *stream);
 
 /* Kernel timing on the engine's launch stream (HIP events around every launch
  * of the assign kernel and of the candidate and tail kernels).  enable=1 starts
