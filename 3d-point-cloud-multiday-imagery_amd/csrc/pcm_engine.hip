@@ -68,8 +68,8 @@ struct pcm_engine {
     int zlev = 0;
     float4 *tbox = nullptr;          // [tile][2] exact point box
     uint32_t *tl_cnt = nullptr;      // [tile] list length (tiles of FULL cells) or FULL
-    float4 *tl_rec = nullptr;        // [tile][CAPF]
-    int32_t *tl_lab = nullptr;       // [tile][CAPF]
+    float4 *tl_rec = nullptr;        // [tile][TLCAP]
+    int32_t *tl_lab = nullptr;       // [tile][TLCAP]
     uint32_t *zcnt = nullptr;        // occupancy sample counts [ncells + 1]
     size_t cap_tbox = 0, cap_tlc = 0, cap_tlr = 0, cap_tll = 0, cap_zcnt = 0;
     uint32_t *perm = nullptr;
@@ -442,7 +442,7 @@ static unsigned cell_bits(long long nc) {
 }
 
 // Crowded-cell detection (tile lists, k_tile_cand): the cell counts of a strided
-// sample of up to 2^22 points, scaled to n.  A cell expected to hold more than
+// sample of up to 2^20 points, scaled to n.  A cell expected to hold more than
 // ZCROWD tiles' worth of points gets its points ordered by zlev Morton levels,
 // enough that a level-zlev box of the fullest cell holds ~1/8 tile (the lists
 // are only needed when K exceeds CAPF).  One host read-back of 4 bytes.
@@ -459,7 +459,7 @@ static int choose_zlev(pcm_engine *e, const void *X, hipStream_t s) {
     }
     constexpr double ZCROWD = 4.0;
     if (!e->g.prune || e->k <= CAPF || n < (long long)(ZCROWD * e->tile_cap) || zmax < 1) return 0;
-    const long long m = std::min(n, 1LL << 22), stride = n / m;
+    const long long m = std::min(n, 1LL << 20), stride = n / m;
     HIPCHK(ensure(e->zcnt, e->cap_zcnt, (size_t)(nc + 1) * sizeof(uint32_t)));
     HIPCHK(hipMemsetAsync(e->zcnt, 0, (size_t)(nc + 1) * sizeof(uint32_t), s));
     int rc = dispatch_td(e->dtype, d, [&](auto T, auto DD) -> int {
@@ -629,8 +629,8 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     if (e->zlev > 0) {   // crowded layout: exact tile boxes and tile-list storage
         HIPCHK(ensure(e->tbox, e->cap_tbox, (size_t)e->ntiles_cap * 2 * sizeof(float4)));
         HIPCHK(ensure(e->tl_cnt, e->cap_tlc, (size_t)e->ntiles_cap * sizeof(uint32_t)));
-        HIPCHK(ensure(e->tl_rec, e->cap_tlr, (size_t)e->ntiles_cap * CAPF * sizeof(float4)));
-        HIPCHK(ensure(e->tl_lab, e->cap_tll, (size_t)e->ntiles_cap * CAPF * sizeof(int32_t)));
+        HIPCHK(ensure(e->tl_rec, e->cap_tlr, (size_t)e->ntiles_cap * TLCAP * sizeof(float4)));
+        HIPCHK(ensure(e->tl_lab, e->cap_tll, (size_t)e->ntiles_cap * TLCAP * sizeof(int32_t)));
         rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
             using TT = decltype(T);
             constexpr int D = decltype(DD)::value;
@@ -849,7 +849,7 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
                         A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
                 else
                     k_lloyd1<TT, D, LS, (D <= 3 && LS == LSLOT)><<<lloyd_grid(e), TPB, lds, s>>>(
-                        A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
+                        A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt, e->zlev > 0 ? e->tl_rec : e->C);
             };
             // coarse grids keep 16 slots with masks: 8 slots + LDS int64 words 42.0 -> 51.2 us,
             // 12 slots + global atomics 42.6 -> 65.7 us at 12.5M (tools/mls_sweep.sh)
@@ -1171,12 +1171,12 @@ int pcm_candidate_stats(pcm_engine *e, double *mean, int *mx, int64_t *full_cell
     return 0;
 }
 
-int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *full_tiles, int64_t *listed_tiles, int64_t *listed_len,
+int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *crowded_tiles, int64_t *listed_tiles, int64_t *listed_len,
                         void *stream) {
-    if (!e || !zlev || !full_tiles || !listed_tiles || !listed_len) return fail(PCM_E_ARG, "bad argument");
+    if (!e || !zlev || !crowded_tiles || !listed_tiles || !listed_len) return fail(PCM_E_ARG, "bad argument");
     if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
     *zlev = e->zlev;
-    *full_tiles = *listed_tiles = *listed_len = 0;
+    *crowded_tiles = *listed_tiles = *listed_len = 0;
     if (e->zlev <= 0 || e->n == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipMemsetAsync(e->cand_stats, 0, 3 * sizeof(unsigned long long), s));
@@ -1186,7 +1186,7 @@ int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *full_tiles, int64_t *
     unsigned long long h[3];
     HIPCHK(hipMemcpyAsync(h, e->cand_stats, sizeof(h), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    *full_tiles = (int64_t)h[0];
+    *crowded_tiles = (int64_t)h[0];
     *listed_tiles = (int64_t)h[1];
     *listed_len = (int64_t)h[2];
     return 0;

@@ -33,6 +33,8 @@ constexpr int TILE = 32 * TPB;     // max points per tile: <= 32 per lane, 64 pe
 // to 2 blocks/CU and k_global + k_cand is faster (K = 4096, D = 4: 241 vs 439 us)
 constexpr int KSTEP_MAX = 2048;
 constexpr uint32_t FULL = 0xFFFFFFFFu;
+constexpr int TLCAP = 256;        // tile-list capacity (lists past CAPF are scanned from global memory)
+constexpr uint32_t TL_MIN = 16;   // crowded layouts: tiles of cells with longer lists (or FULL) get tile lists
 constexpr int QBITS = 25;
 // Pruning margins (see DESIGN.md "Exactness of pruning").
 constexpr double PEPS = 7.62939453125e-06;   // 2^-17  >> 6 * 2^-24 (fp32 distance error)
@@ -523,12 +525,13 @@ __global__ __launch_bounds__(256) void k_tile_box(const T *__restrict__ xs, cons
     }
 }
 
-// List of one tile of a FULL cell over its point box, at the current centres:
+// List of one tile of a crowded cell (list FULL or longer than TL_MIN) over its
+// point box, at the current centres:
 // reference r = a centre of least max distance to the box, then every centre
 // not provably dominated by r (prunable), compacted in ascending centroid index
 // (the strict-'<' scan keeps the lowest index on ties).  tl_cnt[t] = the length,
-// or FULL past CAPF (the tile scans all K).  Tiles of other cells are skipped
-// (k_lloyd1 reads tl_cnt only for FULL cells).
+// or FULL when it is not shorter than the cell's list or exceeds CAPF.  Tiles of
+// other cells are skipped (k_lloyd1 reads tl_cnt only for cells past TL_MIN).
 template <int D>
 __global__ __launch_bounds__(256) void k_tile_cand(const uint4 *__restrict__ tiles, const uint32_t *__restrict__ ntiles,
                                                    const uint32_t *__restrict__ fc_cnt, const float4 *__restrict__ tbox,
@@ -539,7 +542,8 @@ __global__ __launch_bounds__(256) void k_tile_cand(const uint4 *__restrict__ til
     if (gate && gated(ctrl)) return;
     if (t >= *ntiles) return;
     const uint4 tr = tiles[t];
-    if (fc_cnt[tr.x] != FULL) return;
+    const uint32_t cc = fc_cnt[tr.x];
+    if (cc <= TL_MIN) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const float4 lo4 = tbox[2 * (size_t)t], hi4 = tbox[2 * (size_t)t + 1];
     double blo[MAXD], bhi[MAXD];
@@ -579,18 +583,19 @@ __global__ __launch_bounds__(256) void k_tile_cand(const uint4 *__restrict__ til
             total += s_w[w];
         }
         const unsigned pos = off + (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
-        if (keep && pos < (unsigned)CAPF) {
-            tl_rec[(size_t)t * CAPF + pos] = C[j];
-            tl_lab[(size_t)t * CAPF + pos] = j;
+        if (keep && pos < (unsigned)TLCAP) {
+            tl_rec[(size_t)t * TLCAP + pos] = C[j];
+            tl_lab[(size_t)t * TLCAP + pos] = j;
         }
         base += total;
         __syncthreads();   // s_w is rewritten by the next chunk
-        if (base > (unsigned)CAPF) break;   // block-uniform
+        if (base > (unsigned)TLCAP) break;   // block-uniform
     }
-    if (tid == 0) tl_cnt[t] = base <= (unsigned)CAPF ? base : FULL;
+    // FULL: no shorter list than the cell's (the tile scans the cell list, or all K)
+    if (tid == 0) tl_cnt[t] = (base <= (unsigned)TLCAP && base < cc) ? base : FULL;
 }
 
-// Tile-list summary: out[0] += tiles of FULL cells, out[1] += those with a
+// Tile-list summary: out[0] += tiles of cells past TL_MIN, out[1] += those with a
 // tile list, out[2] += the lengths of those lists.
 __global__ __launch_bounds__(256) void k_tile_list_stats(const uint4 *__restrict__ tiles,
                                                          const uint32_t *__restrict__ ntiles,
@@ -599,7 +604,7 @@ __global__ __launch_bounds__(256) void k_tile_list_stats(const uint4 *__restrict
                                                          unsigned long long *__restrict__ out) {
     const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (t >= *ntiles) return;
-    if (fc_cnt[tiles[t].x] != FULL) return;
+    if (fc_cnt[tiles[t].x] <= TL_MIN) return;
     atomicAdd(out, 1ull);
     const uint32_t c = tl_cnt[t];
     if (c != FULL) {
@@ -1258,7 +1263,7 @@ struct LloydArgs {
     int sub;                        // the layout is sorted by sub-cell (else sub_start is [ncells + 1])
     Grid g;
     const uint32_t *tl_cnt;         // crowded layouts: per-tile list length for tiles of FULL cells (or FULL), else null
-    const float4 *tl_rec;           // [tile][CAPF] records of the tile lists (k_tile_cand)
+    const float4 *tl_rec;           // [tile][TLCAP] records of the tile lists (k_tile_cand)
     const int32_t *tl_lab;
 };
 
@@ -1333,12 +1338,17 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned 
         tr.w = A.fc_cnt[tr.x];
         const float4 *trec = lrec + (size_t)tr.x * CAPF;
         const int32_t *tlab = llab + (size_t)tr.x * CAPF;
-        if (tr.w == FULL && A.tl_cnt && A.tl_cnt[t] != FULL) {   // crowded cell: the tile's own list
-            tr.w = A.tl_cnt[t];
-            trec = A.tl_rec + (size_t)t * CAPF;
-            tlab = A.tl_lab + (size_t)t * CAPF;
+        const float4 *Cs = A.C;             // all-K / long-list scans read these records
+        const int32_t *glab = nullptr;      // long tile list: position -> centroid index
+        if (tr.w > TL_MIN && A.tl_cnt && A.tl_cnt[t] != FULL) {   // crowded cell: the tile's own list
+            const uint32_t tc = A.tl_cnt[t];
+            trec = A.tl_rec + (size_t)t * TLCAP;
+            tlab = A.tl_lab + (size_t)t * TLCAP;
+            tr.w = tc;
+            if (tc > (uint32_t)CAPF) { Cs = trec; glab = tlab; }
         }
-        const TileL h = make_tile(tr, A.K);
+        TileL h = make_tile(tr, A.K);
+        if (glab) { h.full = 1; h.mm = (int)tr.w; }
         __syncthreads();
         if (!h.full && tid < h.mm) {
             crec[tid] = trec[tid];
@@ -1354,12 +1364,12 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned 
             unpack_x<D>(cur, x);
             float bd[4];
             int bj[4];
-            if (h.full) scan4<D>(A.C, h.mm, x, bd, bj);
+            if (h.full) scan4<D>(Cs, h.mm, x, bd, bj);
             else scan4<D>(crec, h.mm, x, bd, bj);
             int lbl[4];
             bool v[4];
             for (int e = 0; e < 4; ++e) {
-                lbl[e] = h.full ? bj[e] : cid[bj[e]];
+                lbl[e] = h.full ? (glab ? glab[bj[e]] : bj[e]) : cid[bj[e]];
                 v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
                 if (v[e] && inert_out) inert_add(ilo, ihi, iovf, bd[e], iscale);
             }
@@ -1403,25 +1413,7 @@ __device__ __forceinline__ void scan4_s(const float4 *__restrict__ C, int mm, co
         const float4 c = C[0];
         for (int e = 0; e < 4; ++e) { bd[e] = dist_canon<D>(x[e], c); bj[e] = 0; }
     }
-    // Groups of 8 centres are fetched before any is used, so eight scalar
-    // loads share one latency instead of paying it per centre (FULL tiles
-    // scan all K; measured 20 ms/iter on a 16-cluster K=4096 cloud before).
-    int j = 1;
-    for (; j + 8 <= mm; j += 8) {
-        float4 cg[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) cg[u] = C[j + u];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            for (int e = 0; e < 4; ++e) {
-                float dd = dist_canon<D>(x[e], cg[u]);
-                bool lt = dd < bd[e];
-                bd[e] = lt ? dd : bd[e];
-                bj[e] = lt ? j + u : bj[e];
-            }
-        }
-    }
-    for (; j < mm; ++j) {
+    for (int j = 1; j < mm; ++j) {
         const float4 c = C[j];
         for (int e = 0; e < 4; ++e) {
             float dd = dist_canon<D>(x[e], c);
@@ -1698,7 +1690,7 @@ constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !
 template <typename T, int D, int LS, bool MASK>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<T, D, LS, MASK>(), 8))) void k_lloyd1(
     LloydArgs A, const uint4 *__restrict__ tiles, const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
-    const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt) {
+    const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt, const float4 *__restrict__ tl_rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LS+1)*(D+1)][AW]
     __shared__ float4 crec[CAPF];
     __shared__ int32_t cid[CAPF];
@@ -1732,17 +1724,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         l0 = fc_lab[(size_t)cell * CAPF + tid];
     }
     uint32_t cnt = fc_cnt[cell];
-    // crowded cell (FULL list): the tile's own list when k_tile_cand built one
+    // crowded cell (list FULL or past TL_MIN): the tile's own list when k_tile_cand built a shorter one
+    // (lists past CAPF: scanned from global memory like the all-K scan, Cs/glab)
+    // (the all-K and long-list scans read through scalar loads of kernel
+    // arguments: Call / tl_rec, never a selected pointer, which would turn them
+    // into vector loads)
     const float4 *lrec = fc_rec + (size_t)cell * CAPF;
     const int32_t *llab = fc_lab + (size_t)cell * CAPF;
+    const int32_t *glab = nullptr;
     bool tl = false;
-    if (cnt == FULL && A.tl_cnt) {
+    if (cnt > TL_MIN && A.tl_cnt) {
         const uint32_t tc = A.tl_cnt[t];
         if (tc != FULL) {
             cnt = tc;
-            lrec = A.tl_rec + (size_t)t * CAPF;
-            llab = A.tl_lab + (size_t)t * CAPF;
+            lrec = tl_rec + (size_t)t * TLCAP;
+            llab = A.tl_lab + (size_t)t * TLCAP;
             tl = true;
+            if (tc > (uint32_t)CAPF) glab = llab;
         }
     }
     constexpr int NSUB = 1 << D;
@@ -1774,14 +1772,27 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     for (int e = tid; e < AccL<D, LS>::words; e += TPB) acc[e] = 0u;
     if (kOvf)
         for (int e = tid; e < (CAPF - LS) * (D + 1); e += TPB) ovf[e] = 0ull;
-    const bool full = (cnt == FULL);
-    const int mm = full ? A.K : (int)cnt;
+    const bool full = (cnt == FULL) || glab;
+    const int mm = (cnt == FULL) ? A.K : (int)cnt;
+    // long tile list: its centroid indices go to LDS, into crec's bytes (unused
+    // by the global scan: TLCAP int32 = CAPF float4), so the loop's label
+    // lookups stay LDS reads (a vector load there would make the waitcnt pass
+    // drain the point prefetch)
+    static_assert(TLCAP * sizeof(int32_t) <= CAPF * sizeof(float4), "long-list labels fit in crec");
+    int32_t *const glab_s = reinterpret_cast<int32_t *>(&crec[0]);
     if (full) {
-        if (tid < LS) cid[tid] = tid;
+        if (tid < LS) cid[tid] = glab ? (tid < mm ? glab[tid] : 0) : tid;
+        if (glab)
+            for (int j = tid; j < mm; j += TPB) glab_s[j] = glab[j];
     } else {
-        if (tid < LSPEC && tid < mm) {
-            crec[tid] = tl ? lrec[tid] : r0;
-            cid[tid] = tl ? llab[tid] : l0;
+        if (tl) {   // block-uniform: crowded cells only (r0/l0 hold the cell list)
+            if (tid < LSPEC && tid < mm) {
+                crec[tid] = lrec[tid];
+                cid[tid] = llab[tid];
+            }
+        } else if (tid < LSPEC && tid < mm) {
+            crec[tid] = r0;
+            cid[tid] = l0;
         }
         for (int j = LSPEC + tid; j < mm; j += TPB) {   // long lists (rare at D <= 3)
             crec[j] = lrec[j];
@@ -1915,8 +1926,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             }
         } else {
             float bd[4];
-            if (full) scan4_s<D>(Call, mm, x, bd, bj);
-            else scan4<D>(crec, mm, x, bd, bj);
+            if (full) {
+                if (glab) scan4_s<D>(tl_rec + (size_t)t * TLCAP, mm, x, bd, bj);
+                else scan4_s<D>(Call, mm, x, bd, bj);
+            } else {
+                scan4<D>(crec, mm, x, bd, bj);
+            }
         }
         // block-uniform: every point of the round lies inside the tile
         const bool whole = (rbase >= start) && (rbase + 4u * TPB <= end);
@@ -1946,7 +1961,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
                 // one address space per branch (a pointer select would make FLAT
                 // atomics, which count in vmcnt and lgkmcnt and drain the prefetch)
                 if (full || !kOvf) {
-                    unsigned long long *pp = prep + (size_t)(full ? bj[e] : cid[bj[e]]) * (D + 1);
+                    unsigned long long *pp = prep + (size_t)(full ? (glab ? glab_s[bj[e]] : bj[e]) : cid[bj[e]]) * (D + 1);
                     for (int a = 0; a < D; ++a)
                         atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
                     atomicAdd(pp + D, 1ull);

@@ -208,8 +208,8 @@ class Engine:
         z, ft, lt, ll = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         _lib.check(self.lib.pcm_tile_list_stats(self.h, ctypes.byref(z), ctypes.byref(ft), ctypes.byref(lt),
                                                 ctypes.byref(ll), _stream()), "pcm_tile_list_stats")
-        if z.value > 0:   # crowded layout: tiles of FULL cells and their own lists
-            out.update(zlev=z.value, full_tiles=ft.value, listed_tiles=lt.value,
+        if z.value > 0:   # crowded layout: tiles of long-list / FULL cells and their own lists
+            out.update(zlev=z.value, crowded_tiles=ft.value, listed_tiles=lt.value,
                        tile_list_mean=(ll.value / lt.value) if lt.value else 0.0)
         return out
 

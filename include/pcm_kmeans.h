@@ -169,9 +169,10 @@ int pcm_assign_kernel_name(pcm_engine *e, char *buf, size_t n);
 int pcm_candidate_stats(pcm_engine *e, double *mean, int *max, int64_t *full_cells, void *stream);
 /* Crowded layouts (cells holding many tiles' worth of points, e.g. tight
  * clusters): the Morton levels of the in-cell point order (0: not crowded),
- * the tiles of FULL cells at the last iteration, how many of them got a tile
- * list and those lists' summed length (synchronising). */
-int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *full_tiles, int64_t *listed_tiles, int64_t *listed_len,
+ * the tiles of cells whose list is FULL or longer than 16 at the last
+ * iteration, how many of them got a shorter tile list and those lists' summed
+ * length (synchronising). */
+int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *crowded_tiles, int64_t *listed_tiles, int64_t *listed_len,
                         void *stream);
 
 /* Kernel timing on the engine's launch stream (HIP events around every launch

@@ -66,8 +66,7 @@ def test_crowded_bitwise(pcm, name, zlev, monkeypatch):
     st = eng.candidate_stats()
     if zlev != "0":
         assert st.get("zlev", 0) > 0, st                 # detected (auto) or forced
-        if st["full_cells"] > 0:
-            assert st["listed_tiles"] > 0, st            # FULL cells' tiles got their own lists
+        assert st["crowded_tiles"] > 0 and st["listed_tiles"] > 0, st   # long-list cells' tiles got their own lists
     else:
         assert "zlev" not in st
     ref = R.lloyd_fit(X, C0, max_iter=12, tol=0.0, fast=True)
