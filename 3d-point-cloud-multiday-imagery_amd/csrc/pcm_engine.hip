@@ -843,13 +843,18 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
             // else 16 (12.5M-point shard: lists of ~6, 53 vs 57 us)
             auto launch = [&](auto LSc) {
                 constexpr int LS = decltype(LSc)::value;
-                const size_t lds = (size_t)AccL<D, LS>::words * sizeof(uint32_t);
+                // crowded layouts: + the long tile lists' int64 words (AccL::gwords)
+                const size_t lds = e->zlev > 0 ? AccL<D, LS>::bytes_crowded
+                                                : (size_t)AccL<D, LS>::words * sizeof(uint32_t);
                 if (std::getenv("PCM_ASSIGN_BLOCKS_PER_CU"))   // persistent tile walk (tuning sweeps only)
                     k_lloyd<TT, D, LS><<<assign_grid(e, (const void *)k_lloyd<TT, D, LS>, lds), TPB, lds, s>>>(
                         A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
+                else if (e->zlev > 0)   // crowded layout (sub-cell masks off: e->sub = 0)
+                    k_lloyd1<TT, D, LS, false, true><<<lloyd_grid(e), TPB, lds, s>>>(
+                        A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt, e->tl_rec);
                 else
                     k_lloyd1<TT, D, LS, (D <= 3 && LS == LSLOT)><<<lloyd_grid(e), TPB, lds, s>>>(
-                        A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt, e->zlev > 0 ? e->tl_rec : e->C);
+                        A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt, e->C);
             };
             // coarse grids keep 16 slots with masks: 8 slots + LDS int64 words 42.0 -> 51.2 us,
             // 12 slots + global atomics 42.6 -> 65.7 us at 12.5M (tools/mls_sweep.sh)
@@ -1148,9 +1153,9 @@ int pcm_assign_kernel_name(pcm_engine *e, char *buf, size_t n) {
     if (!e || !buf || n == 0) return fail(PCM_E_ARG, "bad argument");
     if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
     const int ls = (e->d <= 3 && lloyd_slots(e) == 8) ? 8 : LSLOT;
-    const bool mask = e->d <= 3 && ls == LSLOT;
-    std::snprintf(buf, n, "k_lloyd1<%s,%d,%d,%s>", e->dtype == PCM_F16 ? "__half" : "float", e->d, ls,
-                  mask ? "true" : "false");
+    const bool mask = e->d <= 3 && ls == LSLOT && e->zlev == 0;
+    std::snprintf(buf, n, "k_lloyd1<%s,%d,%d,%s%s>", e->dtype == PCM_F16 ? "__half" : "float", e->d, ls,
+                  mask ? "true" : "false", e->zlev > 0 ? ",crowded" : "");
     return 0;
 }
 

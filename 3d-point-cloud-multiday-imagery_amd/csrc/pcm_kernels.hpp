@@ -1241,6 +1241,12 @@ constexpr int AW = TPB >= 128 ? TPB / 2 : TPB;   // one wave per block: no shari
 template <int D, int LS = LSLOT> struct AccL {
     static constexpr int rows = (LS + 1) * (D + 1);   // + junk slot
     static constexpr int words = AW * rows;
+    // crowded layouts launch k_lloyd1 with this much more dynamic LDS: int64
+    // words of long tile lists' positions (LDS atomics, one global atomic per
+    // word and tile at the end instead of one per point: contended global
+    // atomics made a 16-cluster K = 4096 cloud L2-atomic-bound)
+    static constexpr int gwords = TLCAP * (D + 1);
+    static constexpr size_t bytes_crowded = ((size_t)words * 4 + 7) / 8 * 8 + (size_t)gwords * 8;
 };
 
 struct LloydArgs {
@@ -1687,7 +1693,9 @@ constexpr int MASK_MIN = PCM_MASK_MIN;   // sub-cell masks for lists of at least
 template <typename T, int D, int LS, bool MASK>
 constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? 6 : PCM_WPE; }
 
-template <typename T, int D, int LS, bool MASK>
+// CROWD: the crowded-layout instance (tile lists, long lists, AccL::gwords of
+// dynamic LDS); the other instances compile without that code.
+template <typename T, int D, int LS, bool MASK, bool CROWD = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<T, D, LS, MASK>(), 8))) void k_lloyd1(
     LloydArgs A, const uint4 *__restrict__ tiles, const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
     const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt, const float4 *__restrict__ tl_rec) {
@@ -1733,7 +1741,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     const int32_t *llab = fc_lab + (size_t)cell * CAPF;
     const int32_t *glab = nullptr;
     bool tl = false;
-    if (cnt > TL_MIN && A.tl_cnt) {
+    if (CROWD && cnt > TL_MIN) {
         const uint32_t tc = A.tl_cnt[t];
         if (tc != FULL) {
             cnt = tc;
@@ -1770,6 +1778,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     ldx(xa, item_off(0));
     ldx(xb, item_off(1));
     for (int e = tid; e < AccL<D, LS>::words; e += TPB) acc[e] = 0u;
+    // long tile lists: block-shared int64 words per list position (AccL::gwords, crowded launches only)
+    unsigned long long *const govf =
+        reinterpret_cast<unsigned long long *>(acc + (AccL<D, LS>::words + 1) / 2 * 2);
     if (kOvf)
         for (int e = tid; e < (CAPF - LS) * (D + 1); e += TPB) ovf[e] = 0ull;
     const bool full = (cnt == FULL) || glab;
@@ -1782,8 +1793,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     int32_t *const glab_s = reinterpret_cast<int32_t *>(&crec[0]);
     if (full) {
         if (tid < LS) cid[tid] = glab ? (tid < mm ? glab[tid] : 0) : tid;
-        if (glab)
+        if (glab) {
             for (int j = tid; j < mm; j += TPB) glab_s[j] = glab[j];
+            for (int j = tid; j < mm * (D + 1); j += TPB) govf[j] = 0ull;
+        }
     } else {
         if (tl) {   // block-uniform: crowded cells only (r0/l0 hold the cell list)
             if (tid < LSPEC && tid < mm) {
@@ -1960,8 +1973,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
                 if (!(v && bj[e] >= LS)) continue;
                 // one address space per branch (a pointer select would make FLAT
                 // atomics, which count in vmcnt and lgkmcnt and drain the prefetch)
-                if (full || !kOvf) {
-                    unsigned long long *pp = prep + (size_t)(full ? (glab ? glab_s[bj[e]] : bj[e]) : cid[bj[e]]) * (D + 1);
+                if (glab) {   // long tile list: block-shared words, folded at the end
+                    unsigned long long *pp = govf + bj[e] * (D + 1);
+                    for (int a = 0; a < D; ++a) atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                    atomicAdd(pp + D, 1ull);
+                } else if (full || !kOvf) {
+                    unsigned long long *pp = prep + (size_t)(full ? bj[e] : cid[bj[e]]) * (D + 1);
                     for (int a = 0; a < D; ++a)
                         atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
                     atomicAdd(pp + D, 1ull);
@@ -2010,6 +2027,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
                 atomicAdd(prep + (size_t)cid[slot] * (D + 1) + qq, (unsigned long long)sacc);
             }
         }
+        if (glab)
+            for (int i = LS * (D + 1) + tid; i < mm * (D + 1); i += TPB) {
+                const unsigned long long w = govf[i];
+                if (w) atomicAdd(prep + (size_t)glab_s[i / (D + 1)] * (D + 1) + i % (D + 1), w);
+            }
         if (kOvf && !full && mm > LS)
             for (int i = tid; i < (mm - LS) * (D + 1); i += TPB) {
                 const unsigned long long w = ovf[i];
