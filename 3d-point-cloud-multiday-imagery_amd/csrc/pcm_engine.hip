@@ -561,40 +561,60 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     // LDS-privatised histogram 0.39 ms + 7.55 ms for its scatter (single-point
     // writes into 32768 key ranges do not merge), vs 1.4 ms sort + 2.9 ms gather
     // (DESIGN.md §3).
-    size_t sort_bytes = 0, scan_bytes = 0;
     unsigned bits = 1;
     while ((1LL << bits) < nsub) ++bits;
     if (e->zlev > 0) bits = cell_bits(nc) + (unsigned)(e->d * e->zlev);   // <= 32 (choose_zlev)
-    if (rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                  (uint32_t *)nullptr, (size_t)n, 0u, bits, s) != hipSuccess ||
-        rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)nc,
+    // PCM_LAYOUT_SORT=0: (key, row) pairs + random row gather (A/B measurement only)
+    static const bool rec_sort = [] {
+        const char *v = std::getenv("PCM_LAYOUT_SORT");
+        return !(v && std::atoi(v) == 0);
+    }();
+    uint32_t *keys2 = nullptr, *tcnt = nullptr;
+    void *tmp = nullptr;
+    size_t scan_bytes = 0;
+    if (rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)nc,
                                 rocprim::plus<uint32_t>(), s) != hipSuccess)
         return fail(PCM_E_HIP, "layout: rocprim size query failed");
-    const size_t o_keys = 0, o_keys2 = align_up(o_keys + n * 4), o_vals = align_up(o_keys2 + n * 4),
-                 o_tcnt = align_up(o_vals + n * 4), o_tmp = align_up(o_tcnt + nc * 4),
-                 ws_need = o_tmp + std::max(sort_bytes, scan_bytes);
-    if (ensure(e->ws, e->cap_ws, ws_need) != hipSuccess) return fail(PCM_E_NOMEM, "layout scratch");
-    char *wb = (char *)e->ws;
-    uint32_t *keys = (uint32_t *)(wb + o_keys), *keys2 = (uint32_t *)(wb + o_keys2), *vals = (uint32_t *)(wb + o_vals),
-             *tcnt = (uint32_t *)(wb + o_tcnt);
-    void *tmp = wb + o_tmp;
-
     int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
-        k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, e->zlev, keys, vals);
-        LAUNCHCHK();
-        return 0;
-    });
-    if (rc) return rc;
-    size_t tb = sort_bytes;
-    if (hipError_t err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))
-        return fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
-    rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-        using TT = decltype(T);
-        constexpr int D = decltype(DD)::value;
-        k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs);
-        LAUNCHCHK();
+        using R = PRec<TT, D>;
+        const size_t vsz = rec_sort ? sizeof(R) : sizeof(uint32_t);
+        size_t sort_bytes = 0;
+        hipError_t qe = rec_sort ? rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr,
+                                                              (uint32_t *)nullptr, (R *)nullptr, (R *)nullptr,
+                                                              (size_t)n, 0u, bits, s)
+                                 : rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr,
+                                                              (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                              (uint32_t *)nullptr, (size_t)n, 0u, bits, s);
+        if (qe != hipSuccess) return fail(PCM_E_HIP, "layout: rocprim size query failed");
+        const size_t o_keys = 0, o_keys2 = align_up(o_keys + n * 4), o_vals = align_up(o_keys2 + n * 4),
+                     o_vals2 = align_up(o_vals + n * vsz), o_tcnt = align_up(o_vals2 + (rec_sort ? n * vsz : 0)),
+                     o_tmp = align_up(o_tcnt + nc * 4), ws_need = o_tmp + std::max(sort_bytes, scan_bytes);
+        if (ensure(e->ws, e->cap_ws, ws_need) != hipSuccess) return fail(PCM_E_NOMEM, "layout scratch");
+        char *wb = (char *)e->ws;
+        uint32_t *keys = (uint32_t *)(wb + o_keys);
+        keys2 = (uint32_t *)(wb + o_keys2);
+        tcnt = (uint32_t *)(wb + o_tcnt);
+        tmp = wb + o_tmp;
+        size_t tb = sort_bytes;
+        if (rec_sort) {
+            R *recs = (R *)(wb + o_vals), *recs2 = (R *)(wb + o_vals2);
+            k_subcellid_rec<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, e->zlev, keys, recs);
+            LAUNCHCHK();
+            if (hipError_t err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, recs, recs2, (size_t)n, 0u, bits, s))
+                return fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
+            k_rec_place<TT, D><<<blocks_for(e->npad), 256, 0, s>>>(recs2, n, e->npad, e->perm, (TT *)e->xs);
+            LAUNCHCHK();
+        } else {
+            uint32_t *vals = (uint32_t *)(wb + o_vals);
+            k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, e->zlev, keys, vals);
+            LAUNCHCHK();
+            if (hipError_t err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))
+                return fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
+            k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs);
+            LAUNCHCHK();
+        }
         return 0;
     });
     if (rc) return rc;
@@ -1251,8 +1271,8 @@ int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int 
 // device memory comes from the caller's workspace (pcm_kmeanspp_workspace).
 namespace {
 struct KppWs {   // byte offsets into the workspace
-    size_t bbox_part, bbox_out, nonfinite, keys, keys2, vals, perm, inv, xs, closest, cell_start, cmax, bsum, ctl,
-        um, tmp, total;
+    size_t bbox_part, bbox_out, nonfinite, keys, keys2, recs, recs2, perm, crow, xs, closest, cell_start, cmax, bsum,
+        ctl, um, tmp, total;
     long long nc_max;
     size_t sort_bytes;
 };
@@ -1267,8 +1287,13 @@ int kpp_layout(long long n, int d, int k, int L, KppWs &w) {
     const long long nb = (n + KPP_OB - 1) / KPP_OB;
     w.nc_max = kpp_cells_max(n, d);
     w.sort_bytes = 0;
-    if (rocprim::radix_sort_pairs(nullptr, w.sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                  (uint32_t *)nullptr, (size_t)n, 0u, 21u, (hipStream_t)0) != hipSuccess)
+    const size_t rsz = (size_t)(d + 1) * 4;   // sizeof(PRec<float, d>)
+    if (dispatch_d(d, [&](auto DD) -> int {
+            constexpr int D = decltype(DD)::value;
+            using R = PRec<float, D>;
+            return rocprim::radix_sort_pairs(nullptr, w.sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (R *)nullptr, (R *)nullptr, (size_t)n, 0u, 21u, (hipStream_t)0) != hipSuccess;
+        }))
         return fail(PCM_E_HIP, "kmeanspp sort size query");
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t at = o; o = align_up(o + std::max<size_t>(bytes, 8)); return at; };
@@ -1277,9 +1302,10 @@ int kpp_layout(long long n, int d, int k, int L, KppWs &w) {
     w.nonfinite = take(sizeof(unsigned));
     w.keys = take(n * 4);
     w.keys2 = take(n * 4);
-    w.vals = take(n * 4);
+    w.recs = take(n * rsz);
+    w.recs2 = take(n * rsz);
     w.perm = take(n * 4);
-    w.inv = take(n * 4);
+    w.crow = take(n * 4);
     w.xs = take((size_t)npad * d * sizeof(float));
     w.closest = take(n * 4);
     w.cell_start = take((w.nc_max + 1) * 4);
@@ -1328,9 +1354,9 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
           *cmax = (float *)(wb + w.cmax);
     double *bbox_out = (double *)(wb + w.bbox_out);
     unsigned *nonfinite = (unsigned *)(wb + w.nonfinite);
-    uint32_t *keys = (uint32_t *)(wb + w.keys), *keys2 = (uint32_t *)(wb + w.keys2), *vals = (uint32_t *)(wb + w.vals),
-             *perm = (uint32_t *)(wb + w.perm), *inv = (uint32_t *)(wb + w.inv),
-             *cell_start = (uint32_t *)(wb + w.cell_start);
+    uint32_t *keys = (uint32_t *)(wb + w.keys), *keys2 = (uint32_t *)(wb + w.keys2),
+             *perm = (uint32_t *)(wb + w.perm), *cell_start = (uint32_t *)(wb + w.cell_start);
+    float *crow = (float *)(wb + w.crow);
     unsigned long long *bsum = (unsigned long long *)(wb + w.bsum), *um = (unsigned long long *)(wb + w.um);
     KppCtl *ctl = (KppCtl *)(wb + w.ctl);
     void *tmp = wb + w.tmp;
@@ -1372,21 +1398,23 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
     HIPCHK(hipMemsetAsync(ctl, 0, sizeof(KppCtl), s));
     return dispatch_d(d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        // cell layout (the Lloyd engine's kernels): cell ids, radix sort, AoSoA-4 gather, cell starts
-        k_cellid<float, D><<<blocks_for(n), 256, 0, s>>>(X, n, g, keys, vals);
+        // cell layout (the Lloyd engine's kernels): cell ids + point records, a
+        // radix sort that moves the records, AoSoA-4 placement, cell starts
+        using R = PRec<float, D>;
+        R *recs = (R *)(wb + w.recs), *recs2 = (R *)(wb + w.recs2);
+        k_subcellid_rec<float, D><<<blocks_for(n), 256, 0, s>>>(X, n, g, 0, 0, keys, recs);
         LAUNCHCHK();
         size_t tb = w.sort_bytes;
-        if (hipError_t e2 = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, perm, (size_t)n, 0u, bits, s))
+        if (hipError_t e2 = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, recs, recs2, (size_t)n, 0u, bits, s))
             return fail(PCM_E_HIP, std::string("kmeanspp sort: ") + hipGetErrorString(e2));
-        k_gather<float, D><<<blocks_for(npad), 256, 0, s>>>(X, n, npad, perm, xs);
+        k_rec_place<float, D><<<blocks_for(npad), 256, 0, s>>>(recs2, n, npad, perm, xs);
         LAUNCHCHK();
         k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, cell_start);
         LAUNCHCHK();
-        k_inverse_perm<<<blocks_for(n), 256, 0, s>>>(perm, n, inv);
-        LAUNCHCHK();
         const int pgrid = ncu * 8;
-        k_kpp_init<D><<<pgrid, 256, 0, s>>>(xs, perm, cell_start, nc, X, first_index, scale, closest, cmax, bsum, ctl,
-                                            (long long *)indices);
+        k_kpp_init<D><<<pgrid, 256, 0, s>>>(xs, cell_start, nc, X, first_index, closest, cmax, (long long *)indices);
+        LAUNCHCHK();
+        k_kpp_init_rows<D><<<(int)std::min<long long>(nb, pgrid), 256, 0, s>>>(X, n, first_index, scale, crow, bsum, ctl);
         LAUNCHCHK();
         // from centre 64 on a step touches a neighbourhood: a quarter of the grid
         // (2048 -> 512 blocks) for eval/apply, 163.3 -> 159.1 ms at config 3
@@ -1395,13 +1423,13 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
         static const int late_c = [] { const char *v = std::getenv("PCM_KPP_LATE_C"); return v ? std::atoi(v) : 64; }();
         for (int c = 1; c < k; ++c) {
             const int eg = c >= late_c ? std::max(ncu, pgrid / late_div) : pgrid;
-            k_kpp_search<D><<<L + KPP_RED_BLOCKS, KPP_STPB, 0, s>>>(bsum, nb, closest, inv, X, n,
+            k_kpp_search<D><<<L + KPP_RED_BLOCKS, KPP_STPB, 0, s>>>(bsum, nb, crow, X, n,
                                                                     um + (size_t)(c - 1) * L, L, scale, c, cmax, nc,
                                                                     ctl);
             LAUNCHCHK();
             k_kpp_eval<D><<<eg, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
             LAUNCHCHK();
-            k_kpp_apply<D><<<eg, 256, 0, s>>>(xs, perm, cell_start, g, closest, cmax, bsum, L, scale, c,
+            k_kpp_apply<D><<<eg, 256, 0, s>>>(xs, perm, cell_start, g, closest, crow, cmax, bsum, L, scale, c,
                                               c + 1 < k ? 1 : 0, (long long *)indices, ctl);
             LAUNCHCHK();
         }

@@ -289,6 +289,27 @@ __global__ __launch_bounds__(256) void k_subcellid(const T *__restrict__ X, long
     vals[i] = (uint32_t)i;
 }
 
+// Point record carried through the layout sort (coordinates + caller row), so
+// that the sort itself moves the points and no random row gather follows.
+template <typename T, int D> struct PRec {
+    T c[D];
+    uint32_t row;
+};
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_subcellid_rec(const T *__restrict__ X, long long n, Grid g, int with_sub,
+                                                       int zlev, uint32_t *__restrict__ keys,
+                                                       PRec<T, D> *__restrict__ recs) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = sort_key<T, D>(X, i, g, with_sub, zlev);
+    PRec<T, D> r;
+#pragma unroll
+    for (int a = 0; a < D; ++a) r.c[a] = X[i * D + a];
+    r.row = (uint32_t)i;
+    recs[i] = r;
+}
+
 // cell_start[c] = sub_start[c << d], c in [0, ncells]
 __global__ __launch_bounds__(256) void k_cell_from_sub(const uint32_t *__restrict__ sub_start, long long ncells, int d,
                                                        uint32_t *__restrict__ cell_start) {
@@ -317,6 +338,23 @@ __global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long lo
     const long long src = i < n ? (long long)perm[i] : -1;
 #pragma unroll
     for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = src >= 0 ? X[src * D + a] : (T)0.0f;
+}
+
+// Sorted records -> AoSoA-4 `xs` + `perm` (sequential read, coalesced writes).
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_rec_place(const PRec<T, D> *__restrict__ recs, long long n, long long npad,
+                                                   uint32_t *__restrict__ perm, T *__restrict__ xs) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= npad) return;
+    if (i < n) {
+        const PRec<T, D> r = recs[i];
+        perm[i] = r.row;
+#pragma unroll
+        for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = r.c[a];
+    } else {
+#pragma unroll
+        for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = (T)0.0f;
+    }
 }
 
 // cell_start[c] = first sorted index with key >= c, for c in [0, ncells]

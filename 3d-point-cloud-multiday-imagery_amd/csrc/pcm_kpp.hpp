@@ -14,7 +14,8 @@
 //   k_kpp_search  L blocks: target t's original-order weight block by an exact
 //                 prefix over the block sums `bsum`, then the first row of that
 //                 block whose inclusive prefix reaches the target (searchsorted
-//                 side='left'); extra blocks reduce the per-cell maxima of
+//                 side='left'; the rows' weights from `crow`, the caller-order
+//                 copy of the closest distances); extra blocks reduce the per-cell maxima of
 //                 `closest` to gmax (a bound on every point's closest distance)
 //   k_kpp_eval    per candidate, the potential drop sum_i w(closest_i) -
 //                 w(min(closest_i, d(x_i, cand))) over the cells the candidate
@@ -178,24 +179,24 @@ __device__ __forceinline__ void kpp_cell_points(const float *__restrict__ xs, co
     }
 }
 
-// Step 0: closest := d(x, c0) for every point, cell maxima, original-order
-// block sums of the weights and the potential.  One wave per cell (strided).
+__device__ __forceinline__ float4 kpp_row_centre(const float *__restrict__ X, long long r, int D) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < D; ++a) v[a] = X[r * D + a];
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// Step 0, cell order: closest := d(x, c0) for every point and the cell maxima.
+// One wave per cell (strided).
 template <int D>
-__global__ __launch_bounds__(256) void k_kpp_init(const float *__restrict__ xs, const uint32_t *__restrict__ perm,
-                                                  const uint32_t *__restrict__ cell_start, long long ncells,
-                                                  const float *__restrict__ X, long long first, int s,
+__global__ __launch_bounds__(256) void k_kpp_init(const float *__restrict__ xs, const uint32_t *__restrict__ cell_start,
+                                                  long long ncells, const float *__restrict__ X, long long first,
                                                   float *__restrict__ closest, float *__restrict__ cmax,
-                                                  unsigned long long *__restrict__ bsum, KppCtl *__restrict__ ctl,
                                                   long long *__restrict__ indices) {
     if (blockIdx.x == 0 && threadIdx.x == 0) indices[0] = first;
-    float c0v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int a = 0; a < D; ++a) c0v[a] = X[first * D + a];
-    const float4 c0 = make_float4(c0v[0], c0v[1], c0v[2], c0v[3]);
+    const float4 c0 = kpp_row_centre(X, first, D);
     const int lane = threadIdx.x & 63;
     const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
     const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-    unsigned long long pot = 0ull;
     for (long long cell = wid; cell < ncells; cell += nw) {
         const uint32_t b = cell_start[cell], e = cell_start[cell + 1];
         float mx = 0.f;
@@ -204,16 +205,51 @@ __global__ __launch_bounds__(256) void k_kpp_init(const float *__restrict__ xs, 
             kpp_point<D>(xs, i, x);
             const float d = dist_canon<D>(x, c0);
             closest[i] = d;
-            const unsigned long long w = kpp_w(d, s);
-            pot += w;
-            atomicAdd(&bsum[perm[i] >> KPP_OB_LOG], w);
             mx = fmaxf(mx, d);
         }
         mx = wave_max_f(mx);
         if (lane == 0) cmax[cell] = mx;
     }
-    pot = wave_sum_u64(pot);
-    if (lane == 0 && pot) atomicAdd(&ctl->pot[1], pot);
+}
+
+// Step 0, row order: crow[j] := d(X_j, c0) (the caller-order copy of `closest`
+// that k_kpp_search reads), the weight sum of every KPP_OB-row block (a block
+// reduction, plain store: no atomics) and the potential (one atomic per
+// workgroup).  The same canonical distance as k_kpp_init: bitwise equal values.
+template <int D>
+__global__ __launch_bounds__(256) void k_kpp_init_rows(const float *__restrict__ X, long long n, long long first, int s,
+                                                       float *__restrict__ crow, unsigned long long *__restrict__ bsum,
+                                                       KppCtl *__restrict__ ctl) {
+    __shared__ unsigned long long wtot[4];
+    const float4 c0 = kpp_row_centre(X, first, D);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const long long nb = (n + KPP_OB - 1) / KPP_OB;
+    unsigned long long pot = 0ull;
+    for (long long b = blockIdx.x; b < nb; b += gridDim.x) {
+        unsigned long long acc = 0ull;
+#pragma unroll 4
+        for (int e = 0; e < KPP_OB / 256; ++e) {
+            const long long j = b * KPP_OB + e * 256 + tid;
+            if (j < n) {
+                float x[D];
+#pragma unroll
+                for (int a = 0; a < D; ++a) x[a] = X[j * D + a];
+                const float d = dist_canon<D>(x, c0);
+                crow[j] = d;
+                acc += kpp_w(d, s);
+            }
+        }
+        acc = wave_sum_u64(acc);
+        if (lane == 0) wtot[wv] = acc;
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long t = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+            bsum[b] = t;
+            pot += t;
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && pot) atomicAdd(&ctl->pot[1], pot);
 }
 
 // Inclusive scan of one u64 per thread over a KPP_STPB-thread block: wave
@@ -244,8 +280,7 @@ __device__ __forceinline__ unsigned long long kpp_block_exscan(unsigned long lon
 // target made this launch 45-54 us per centre.
 template <int D>
 __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long long *__restrict__ bsum, long long nb,
-                                                         const float *__restrict__ closest,
-                                                         const uint32_t *__restrict__ inv, const float *__restrict__ X,
+                                                         const float *__restrict__ crow, const float *__restrict__ X,
                                                          long long n, const unsigned long long *__restrict__ umant,
                                                          int L, int s, int c, const float *__restrict__ cmax,
                                                          long long ncells, KppCtl *__restrict__ ctl) {
@@ -339,16 +374,16 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
         constexpr int PER = KPP_OB / KPP_STPB;
         unsigned long long w[PER];
         unsigned long long l2 = 0ull;
-        uint32_t ir[PER];
+        float cr[PER];
 #pragma unroll
         for (int e = 0; e < PER; ++e) {
             const long long j = blk * KPP_OB + (long long)tid * PER + e;
-            ir[e] = j < n ? inv[j] : 0u;
+            cr[e] = j < n ? crow[j] : 0.f;
         }
 #pragma unroll
         for (int e = 0; e < PER; ++e) {
             const long long j = blk * KPP_OB + (long long)tid * PER + e;
-            w[e] = j < n ? kpp_w(closest[ir[e]], s) : 0ull;
+            w[e] = j < n ? kpp_w(cr[e], s) : 0ull;
             l2 += w[e];
         }
         DBG_T(5);
@@ -513,9 +548,9 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
 template <int D>
 __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs, const uint32_t *__restrict__ perm,
                                                    const uint32_t *__restrict__ cell_start, Grid g,
-                                                   float *__restrict__ closest, float *__restrict__ cmax,
-                                                   unsigned long long *__restrict__ bsum, int L, int s, int c,
-                                                   int apply, long long *__restrict__ indices,
+                                                   float *__restrict__ closest, float *__restrict__ crow,
+                                                   float *__restrict__ cmax, unsigned long long *__restrict__ bsum,
+                                                   int L, int s, int c, int apply, long long *__restrict__ indices,
                                                    KppCtl *__restrict__ ctl) {
     const int tid = threadIdx.x, lane = tid & 63;
     const unsigned long long pot = ctl->pot[c & 1];
@@ -563,8 +598,10 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
             kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t i, const float (&x)[D], float cl) {
                 const float d = dist_canon<D>(x, best);
                 if (d < cl) {
+                    const uint32_t r = perm[i];
                     closest[i] = d;
-                    atomicAdd(&bsum[perm[i] >> KPP_OB_LOG], ~(kpp_w(cl, s) - kpp_w(d, s)) + 1ull);   // -= (mod 2^64)
+                    crow[r] = d;
+                    atomicAdd(&bsum[r >> KPP_OB_LOG], ~(kpp_w(cl, s) - kpp_w(d, s)) + 1ull);   // -= (mod 2^64)
                 }
                 mx = fmaxf(mx, fminf(d, cl));
             });
