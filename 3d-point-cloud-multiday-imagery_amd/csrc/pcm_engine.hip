@@ -16,6 +16,7 @@
 
 #include "pcm_kernels.hpp"
 #include "pcm_kpp.hpp"
+#include "pcm_sort.hpp"
 #include "pcm_cloud.hpp"
 #include "pcm_common.hpp"
 #include "pcm_kmeans.h"
@@ -159,6 +160,74 @@ template <typename F>
 int dispatch_l(const pcm_engine *e, F &&f) {
     if (small_labels(e)) return f(uint16_t{});
     return f(int32_t{});
+}
+
+// LSD record sort (pcm_sort.hpp): passes, chunking and workspace offsets.
+struct RsPlan {
+    int npass = 1, wb = 8;
+    long long nblk = 1, ent = RS_DIG;
+    long long nseg = 1;
+    size_t o_ra = 0, o_rb = 0, o_hist = 0, o_goff = 0, o_segb = 0, total = 0;
+};
+
+template <typename TT, int D>
+void rs_plan(long long n, unsigned bits, RsPlan &p) {
+    using R = PRec<TT, D>;
+    constexpr int CH = RsCfg<TT, D>::CH;
+    p.npass = std::max(1, (int)((bits + 7) / 8));
+    p.wb = (int)((bits + p.npass - 1) / p.npass);
+    p.nblk = std::max(1LL, (n + CH - 1) / CH);
+    p.ent = (long long)RS_DIG * p.nblk;
+    p.nseg = (p.nblk + RS_SEG - 1) / RS_SEG;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t at = o; o = (o + std::max<size_t>(bytes, 8) + 255) / 256 * 256; return at; };
+    p.o_ra = take(p.npass >= 2 ? n * sizeof(R) : 0);
+    p.o_rb = take(p.npass >= 3 ? n * sizeof(R) : 0);
+    p.o_hist = take(p.ent * 4);
+    p.o_goff = take(p.ent * 4);
+    p.o_segb = take((size_t)p.nseg * RS_DIG * 4);
+    p.total = o;
+}
+
+// Sort the caller's rows X into cell order: AoSoA-4 xs (zero padded to npad)
+// and perm (sorted position -> row).
+template <typename TT, int D>
+int rs_sort(const TT *X, long long n, long long npad, const Grid &g, int with_sub, int zlev, unsigned bits,
+            const RsPlan &p, char *wb, TT *xs, uint32_t *perm, hipStream_t s) {
+    using R = PRec<TT, D>;
+    R *ra = (R *)(wb + p.o_ra), *rb = (R *)(wb + p.o_rb);
+    uint32_t *hist = (uint32_t *)(wb + p.o_hist), *goff = (uint32_t *)(wb + p.o_goff),
+             *segb = (uint32_t *)(wb + p.o_segb);
+    const int grid = (int)p.nblk;
+    for (int q = 0; q < p.npass; ++q) {
+        const int shift = q * p.wb, width = std::min(p.wb, (int)bits - shift);
+        const bool from_x = q == 0, to_xs = q == p.npass - 1;
+        const R *rin = from_x ? nullptr : (((q - 1) & 1) ? rb : ra);
+        R *rout = to_xs ? nullptr : ((q & 1) ? rb : ra);
+        if (from_x)
+            k_rs_count<TT, D, true><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, hist);
+        else
+            k_rs_count<TT, D, false><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, hist);
+        LAUNCHCHK();
+        k_rs_colscan<<<(int)p.nseg, RS_DIG, 0, s>>>(hist, p.nblk, goff, segb);
+        LAUNCHCHK();
+        k_rs_segscan<<<1, RS_DIG, 0, s>>>(segb, p.nseg);
+        LAUNCHCHK();
+#define PCM_RS_SCATTER(FX, TX)                                                                                      \
+    k_rs_scatter<TT, D, FX, TX><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, goff, segb, rout, \
+                                                        xs, perm)
+        if (from_x && to_xs) PCM_RS_SCATTER(true, true);
+        else if (from_x) PCM_RS_SCATTER(true, false);
+        else if (to_xs) PCM_RS_SCATTER(false, true);
+        else PCM_RS_SCATTER(false, false);
+#undef PCM_RS_SCATTER
+        LAUNCHCHK();
+    }
+    if (npad > n) {
+        k_xs_pad<TT, D><<<1, 64, 0, s>>>(n, npad, xs);
+        LAUNCHCHK();
+    }
+    return 0;
 }
 
 // The layout's buffers persist across layouts (a later cloud reuses them when
@@ -555,21 +624,16 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     if (e->zlev > 0) e->sub = 0;
     const int sh = e->sub ? e->d : 0;
     const long long nsub = nc << sh;
-    // Key order: a radix sort of (key, row) pairs, then a 12-B row gather into
-    // AoSoA-4.  Counting sorts were measured slower at config 3 (100M points,
-    // 32768 keys): global-atomic counters 3.65 ms (count) + 7.35 ms (scatter), an
-    // LDS-privatised histogram 0.39 ms + 7.55 ms for its scatter (single-point
-    // writes into 32768 key ranges do not merge), vs 1.4 ms sort + 2.9 ms gather
-    // (DESIGN.md §3).
+    // Key order: the LSD record sort of pcm_sort.hpp (no random row gather, no
+    // key array).  Measured at config 3: (key, row) pairs sort +
+    // 12-B row gather 1.4 + 2.9 ms; rocprim pairs sort with 16-B point records
+    // as values 3.4 ms in all; counting sorts slower still (global-atomic
+    // counters 3.65 + 7.35 ms, LDS-privatised 0.39 + 7.55 ms: single-point
+    // writes into 32768 key ranges do not merge).
     unsigned bits = 1;
     while ((1LL << bits) < nsub) ++bits;
     if (e->zlev > 0) bits = cell_bits(nc) + (unsigned)(e->d * e->zlev);   // <= 32 (choose_zlev)
-    // PCM_LAYOUT_SORT=0: (key, row) pairs + random row gather (A/B measurement only)
-    static const bool rec_sort = [] {
-        const char *v = std::getenv("PCM_LAYOUT_SORT");
-        return !(v && std::atoi(v) == 0);
-    }();
-    uint32_t *keys2 = nullptr, *tcnt = nullptr;
+    uint32_t *tcnt = nullptr;
     void *tmp = nullptr;
     size_t scan_bytes = 0;
     if (rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)nc,
@@ -578,54 +642,31 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
         using TT = decltype(T);
         constexpr int D = decltype(DD)::value;
-        using R = PRec<TT, D>;
-        const size_t vsz = rec_sort ? sizeof(R) : sizeof(uint32_t);
-        size_t sort_bytes = 0;
-        hipError_t qe = rec_sort ? rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr,
-                                                              (uint32_t *)nullptr, (R *)nullptr, (R *)nullptr,
-                                                              (size_t)n, 0u, bits, s)
-                                 : rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr,
-                                                              (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                              (uint32_t *)nullptr, (size_t)n, 0u, bits, s);
-        if (qe != hipSuccess) return fail(PCM_E_HIP, "layout: rocprim size query failed");
-        const size_t o_keys = 0, o_keys2 = align_up(o_keys + n * 4), o_vals = align_up(o_keys2 + n * 4),
-                     o_vals2 = align_up(o_vals + n * vsz), o_tcnt = align_up(o_vals2 + (rec_sort ? n * vsz : 0)),
-                     o_tmp = align_up(o_tcnt + nc * 4), ws_need = o_tmp + std::max(sort_bytes, scan_bytes);
+        RsPlan p;
+        rs_plan<TT, D>(n, bits, p);
+        const size_t o_tcnt = align_up(p.total), o_tmp = align_up(o_tcnt + nc * 4), ws_need = o_tmp + scan_bytes;
         if (ensure(e->ws, e->cap_ws, ws_need) != hipSuccess) return fail(PCM_E_NOMEM, "layout scratch");
         char *wb = (char *)e->ws;
-        uint32_t *keys = (uint32_t *)(wb + o_keys);
-        keys2 = (uint32_t *)(wb + o_keys2);
         tcnt = (uint32_t *)(wb + o_tcnt);
         tmp = wb + o_tmp;
-        size_t tb = sort_bytes;
-        if (rec_sort) {
-            R *recs = (R *)(wb + o_vals), *recs2 = (R *)(wb + o_vals2);
-            k_subcellid_rec<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, e->zlev, keys, recs);
-            LAUNCHCHK();
-            if (hipError_t err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, recs, recs2, (size_t)n, 0u, bits, s))
-                return fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
-            k_rec_place<TT, D><<<blocks_for(e->npad), 256, 0, s>>>(recs2, n, e->npad, e->perm, (TT *)e->xs);
-            LAUNCHCHK();
-        } else {
-            uint32_t *vals = (uint32_t *)(wb + o_vals);
-            k_subcellid<TT, D><<<blocks_for(n), 256, 0, s>>>((const TT *)X, n, e->g, e->sub, e->zlev, keys, vals);
-            LAUNCHCHK();
-            if (hipError_t err = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, vals, e->perm, (size_t)n, 0u, bits, s))
-                return fail(PCM_E_HIP, std::string("radix_sort: ") + hipGetErrorString(err));
-            k_gather<TT, D><<<blocks_for(e->npad), 256, 0, s>>>((const TT *)X, n, e->npad, e->perm, (TT *)e->xs);
-            LAUNCHCHK();
-        }
+        if (int rc2 = rs_sort<TT, D>((const TT *)X, n, e->npad, e->g, e->sub, e->zlev, bits, p, wb, (TT *)e->xs,
+                                     e->perm, s))
+            return rc2;
+        // cell (or sub-cell) starts by binary search over the sorted points
+        if (e->zlev > 0)   // Morton-ordered cells: the keys' cell bits
+            k_cell_starts_xs<TT, D><<<blocks_for(nc + 1), 256, 0, s>>>((const TT *)e->xs, n, e->g, 0, e->zlev, nc,
+                                                                      e->cell_start, e->d * e->zlev);
+        else
+            k_cell_starts_xs<TT, D><<<blocks_for(nsub + 1), 256, 0, s>>>((const TT *)e->xs, n, e->g, e->sub, 0, nsub,
+                                                                        e->sub_start, 0);
+        LAUNCHCHK();
         return 0;
     });
     if (rc) return rc;
-    if (e->zlev > 0) {   // Morton-ordered cells: cell starts straight from the keys' cell bits
-        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, e->cell_start, e->d * e->zlev);
-    } else {
-        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nsub, e->sub_start);
-        LAUNCHCHK();
+    if (e->zlev == 0) {
         k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, sh, e->cell_start);
+        LAUNCHCHK();
     }
-    LAUNCHCHK();
     k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap);
     LAUNCHCHK();
     size_t sb = scan_bytes;
@@ -1271,10 +1312,9 @@ int pcm_assign_bruteforce(const float *X, int64_t n, int d, const float *C, int 
 // device memory comes from the caller's workspace (pcm_kmeanspp_workspace).
 namespace {
 struct KppWs {   // byte offsets into the workspace
-    size_t bbox_part, bbox_out, nonfinite, keys, keys2, recs, recs2, perm, crow, xs, closest, cell_start, cmax, bsum,
-        ctl, um, tmp, total;
+    size_t bbox_part, bbox_out, nonfinite, sort, perm, crow, xs, closest, cell_start, cmax, bsum, ctl, um, total;
     long long nc_max;
-    size_t sort_bytes;
+    RsPlan plan;   // the cell sort's plan at the largest grid (kpp_cells_max)
 };
 
 long long kpp_cells_max(long long n, int d) {
@@ -1286,24 +1326,18 @@ int kpp_layout(long long n, int d, int k, int L, KppWs &w) {
     const long long npad = ((n + 3) / 4) * 4 + 4;
     const long long nb = (n + KPP_OB - 1) / KPP_OB;
     w.nc_max = kpp_cells_max(n, d);
-    w.sort_bytes = 0;
-    const size_t rsz = (size_t)(d + 1) * 4;   // sizeof(PRec<float, d>)
-    if (dispatch_d(d, [&](auto DD) -> int {
+    if (int rc = dispatch_d(d, [&](auto DD) -> int {
             constexpr int D = decltype(DD)::value;
-            using R = PRec<float, D>;
-            return rocprim::radix_sort_pairs(nullptr, w.sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                             (R *)nullptr, (R *)nullptr, (size_t)n, 0u, 21u, (hipStream_t)0) != hipSuccess;
+            rs_plan<float, D>(n, cell_bits(w.nc_max), w.plan);
+            return 0;
         }))
-        return fail(PCM_E_HIP, "kmeanspp sort size query");
+        return rc;
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t at = o; o = align_up(o + std::max<size_t>(bytes, 8)); return at; };
     w.bbox_part = take((size_t)BBOX_BLOCKS * 2 * MAXD * sizeof(float));
     w.bbox_out = take(2 * MAXD * sizeof(double));
     w.nonfinite = take(sizeof(unsigned));
-    w.keys = take(n * 4);
-    w.keys2 = take(n * 4);
-    w.recs = take(n * rsz);
-    w.recs2 = take(n * rsz);
+    w.sort = take(w.plan.total);
     w.perm = take(n * 4);
     w.crow = take(n * 4);
     w.xs = take((size_t)npad * d * sizeof(float));
@@ -1313,7 +1347,6 @@ int kpp_layout(long long n, int d, int k, int L, KppWs &w) {
     w.bsum = take(nb * 8);
     w.ctl = take(sizeof(KppCtl));
     w.um = take((size_t)std::max(1, (k - 1) * L) * 8);
-    w.tmp = take(w.sort_bytes);
     w.total = o;
     return 0;
 }
@@ -1354,12 +1387,10 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
           *cmax = (float *)(wb + w.cmax);
     double *bbox_out = (double *)(wb + w.bbox_out);
     unsigned *nonfinite = (unsigned *)(wb + w.nonfinite);
-    uint32_t *keys = (uint32_t *)(wb + w.keys), *keys2 = (uint32_t *)(wb + w.keys2),
-             *perm = (uint32_t *)(wb + w.perm), *cell_start = (uint32_t *)(wb + w.cell_start);
+    uint32_t *perm = (uint32_t *)(wb + w.perm), *cell_start = (uint32_t *)(wb + w.cell_start);
     float *crow = (float *)(wb + w.crow);
     unsigned long long *bsum = (unsigned long long *)(wb + w.bsum), *um = (unsigned long long *)(wb + w.um);
     KppCtl *ctl = (KppCtl *)(wb + w.ctl);
-    void *tmp = wb + w.tmp;
     const long long npad = ((n + 3) / 4) * 4 + 4;
     const long long nb = (n + KPP_OB - 1) / KPP_OB;
     int dev = 0, ncu = 256;
@@ -1398,18 +1429,12 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
     HIPCHK(hipMemsetAsync(ctl, 0, sizeof(KppCtl), s));
     return dispatch_d(d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        // cell layout (the Lloyd engine's kernels): cell ids + point records, a
-        // radix sort that moves the records, AoSoA-4 placement, cell starts
-        using R = PRec<float, D>;
-        R *recs = (R *)(wb + w.recs), *recs2 = (R *)(wb + w.recs2);
-        k_subcellid_rec<float, D><<<blocks_for(n), 256, 0, s>>>(X, n, g, 0, 0, keys, recs);
-        LAUNCHCHK();
-        size_t tb = w.sort_bytes;
-        if (hipError_t e2 = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, recs, recs2, (size_t)n, 0u, bits, s))
-            return fail(PCM_E_HIP, std::string("kmeanspp sort: ") + hipGetErrorString(e2));
-        k_rec_place<float, D><<<blocks_for(npad), 256, 0, s>>>(recs2, n, npad, perm, xs);
-        LAUNCHCHK();
-        k_cell_starts<<<blocks_for(n + 1), 256, 0, s>>>(keys2, n, nc, cell_start);
+        // cell layout (the Lloyd engine's record sort, pcm_sort.hpp), cell starts
+        RsPlan p;
+        rs_plan<float, D>(n, bits, p);
+        if (p.total > w.plan.total) return fail(PCM_E_STATE, "kmeanspp: sort plan exceeds the workspace bound");
+        if (int rc2 = rs_sort<float, D>(X, n, npad, g, 0, 0, bits, p, wb + w.sort, xs, perm, s)) return rc2;
+        k_cell_starts_xs<float, D><<<blocks_for(nc + 1), 256, 0, s>>>(xs, n, g, 0, 0, nc, cell_start, 0);
         LAUNCHCHK();
         const int pgrid = ncu * 8;
         k_kpp_init<D><<<pgrid, 256, 0, s>>>(xs, cell_start, nc, X, first_index, closest, cmax, (long long *)indices);
@@ -1444,6 +1469,10 @@ int pcm_debug_timing(unsigned long long *out, int nblocks) {
 }
 int pcm_debug_timing_eval(unsigned long long *out, int nblocks) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_e), (size_t)nblocks * 8 * sizeof(unsigned long long)));
+    return 0;
+}
+int pcm_debug_kpp_counts(unsigned long long *out, int ncentres) {
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_kpp), (size_t)ncentres * 4 * sizeof(unsigned long long)));
     return 0;
 }
 int pcm_debug_timing_lloyd(unsigned long long *out, int nblocks) {

@@ -7,8 +7,8 @@
 //   k_label            final E-step: labels + inertia (_kmeans.py:736-750)
 //   k_global           averaging / shift / convergence (_k_means_common.pyx:274-311,
 //                      _kmeans.py:717-732)
-// Layout (once per cloud): k_bbox*, k_cellid, rocprim radix sort, k_gather,
-// k_cell_starts, k_tiles.
+// Layout (once per cloud): k_bbox*, the record sort of pcm_sort.hpp (cell
+// order, AoSoA-4), k_cell_starts_xs, k_tiles.
 //
 // Canonical arithmetic (oracle/lloyd_ref.py): fp32 distance
 // ((d0*d0 + d1*d1) + d2*d2) + d3*d3 with every op rounded (-ffp-contract=off),
@@ -227,22 +227,6 @@ __global__ __launch_bounds__(256) void k_bbox_final(const float *__restrict__ pa
         }
 }
 
-template <typename T, int D>
-__global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long long n, Grid g, uint32_t *__restrict__ keys,
-                                                uint32_t *__restrict__ vals) {
-    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int idx[MAXD];
-    for (int a = 0; a < D; ++a) {
-        double t = ((double)to_f<T>(X[i * D + a]) - g.lo[a]) * g.inv[a];
-        int v = (int)floor(t);
-        v = v < 0 ? 0 : (v >= g.G[a] ? g.G[a] - 1 : v);
-        idx[a] = v;
-    }
-    keys[i] = (uint32_t)encode(idx, g.G, D);
-    vals[i] = (uint32_t)i;
-}
-
 // Sort key of the Lloyd layout: the cell id << D | the sub-cell (bit D-1-a set
 // when the point lies in the upper half of its cell along axis a), so that
 // within a cell the points of one sub-cell are contiguous.  The half test uses
@@ -252,22 +236,24 @@ __global__ __launch_bounds__(256) void k_cellid(const T *__restrict__ X, long lo
 // a Morton code of zlev bisections of the cell (level 1 = the sub-cell bits,
 // then the next finer halves, axis 0 first within a level), so the tiles of a
 // crowded cell are compact boxes (tile lists, k_tile_cand).
-template <typename T, int D>
-__device__ __forceinline__ uint32_t sort_key(const T *__restrict__ X, long long i, const Grid &g, int with_sub,
-                                             int zlev) {
+template <int D>
+__device__ __forceinline__ uint32_t sort_key_f(const float (&x)[D], const Grid &g, int with_sub, int zlev) {
     int idx[MAXD];
     uint32_t sub = 0, fz[MAXD];
 #pragma unroll
     for (int a = 0; a < D; ++a) {
-        double t = ((double)to_f<T>(X[i * D + a]) - g.lo[a]) * g.inv[a];
+        double t = ((double)x[a] - g.lo[a]) * g.inv[a];
         int v = (int)floor(t);
         v = v < 0 ? 0 : (v >= g.G[a] ? g.G[a] - 1 : v);
         idx[a] = v;
         const double fr = t - (double)v;
         sub = (sub << 1) | ((fr >= 0.5) ? 1u : 0u);
-        const int top = (1 << zlev) - 1;
-        int m = (int)floor(fr * (double)(1 << zlev));
-        fz[a] = (uint32_t)(m < 0 ? 0 : (m > top ? top : m));
+        fz[a] = 0u;
+        if (zlev > 0) {
+            const int top = (1 << zlev) - 1;
+            int m = (int)floor(fr * (double)(1 << zlev));
+            fz[a] = (uint32_t)(m < 0 ? 0 : (m > top ? top : m));
+        }
     }
     const uint32_t cell = (uint32_t)encode(idx, g.G, D);
     if (zlev > 0) {
@@ -280,35 +266,12 @@ __device__ __forceinline__ uint32_t sort_key(const T *__restrict__ X, long long 
     return with_sub ? (cell << D) | sub : cell;
 }
 
-template <typename T, int D>
-__global__ __launch_bounds__(256) void k_subcellid(const T *__restrict__ X, long long n, Grid g, int with_sub,
-                                                   int zlev, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
-    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    keys[i] = sort_key<T, D>(X, i, g, with_sub, zlev);
-    vals[i] = (uint32_t)i;
-}
-
 // Point record carried through the layout sort (coordinates + caller row), so
 // that the sort itself moves the points and no random row gather follows.
 template <typename T, int D> struct PRec {
     T c[D];
     uint32_t row;
 };
-
-template <typename T, int D>
-__global__ __launch_bounds__(256) void k_subcellid_rec(const T *__restrict__ X, long long n, Grid g, int with_sub,
-                                                       int zlev, uint32_t *__restrict__ keys,
-                                                       PRec<T, D> *__restrict__ recs) {
-    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    keys[i] = sort_key<T, D>(X, i, g, with_sub, zlev);
-    PRec<T, D> r;
-#pragma unroll
-    for (int a = 0; a < D; ++a) r.c[a] = X[i * D + a];
-    r.row = (uint32_t)i;
-    recs[i] = r;
-}
 
 // cell_start[c] = sub_start[c << d], c in [0, ncells]
 __global__ __launch_bounds__(256) void k_cell_from_sub(const uint32_t *__restrict__ sub_start, long long ncells, int d,
@@ -326,61 +289,12 @@ __device__ __forceinline__ long long xs_index(long long i, int a) {
     return ((i >> 2) * D + a) * 4 + (i & 3);
 }
 
-// Gather into cell order (AoSoA-4).  Random 12-B row reads are HBM-line
-// bound; one destination row per thread measured fastest (4 per thread: 3.06
-// vs 2.5 ms at 100M).
-constexpr int GATHER_PER = 1;
-template <typename T, int D>
-__global__ __launch_bounds__(256) void k_gather(const T *__restrict__ X, long long n, long long npad,
-                                                const uint32_t *__restrict__ perm, T *__restrict__ xs) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= npad) return;
-    const long long src = i < n ? (long long)perm[i] : -1;
-#pragma unroll
-    for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = src >= 0 ? X[src * D + a] : (T)0.0f;
-}
-
-// Sorted records -> AoSoA-4 `xs` + `perm` (sequential read, coalesced writes).
-template <typename T, int D>
-__global__ __launch_bounds__(256) void k_rec_place(const PRec<T, D> *__restrict__ recs, long long n, long long npad,
-                                                   uint32_t *__restrict__ perm, T *__restrict__ xs) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= npad) return;
-    if (i < n) {
-        const PRec<T, D> r = recs[i];
-        perm[i] = r.row;
-#pragma unroll
-        for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = r.c[a];
-    } else {
-#pragma unroll
-        for (int a = 0; a < D; ++a) xs[xs_index<D>(i, a)] = (T)0.0f;
-    }
-}
-
-// cell_start[c] = first sorted index with key >= c, for c in [0, ncells]
-// (keys >> shift: the cell ids of Morton-ordered crowded layouts)
-__global__ __launch_bounds__(256) void k_cell_starts(const uint32_t *__restrict__ keys, long long n, long long ncells,
-                                                     uint32_t *__restrict__ start, int shift = 0) {
-    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i > n) return;
-    long long prev = (i == 0) ? -1 : (long long)(keys[i - 1] >> shift);
-    long long cur = (i == n) ? ncells : (long long)(keys[i] >> shift);
-    for (long long c = prev + 1; c <= cur; ++c) start[c] = (uint32_t)i;
-}
-
 __global__ __launch_bounds__(256) void k_tile_counts(const uint32_t *__restrict__ start, long long ncells,
                                                      uint32_t *__restrict__ cnt, uint32_t cap) {
     long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (c >= ncells) return;
     uint32_t n = start[c + 1] - start[c];
     cnt[c] = (n + cap - 1) / cap;
-}
-
-// inv[perm[i]] = i (original row -> sorted position)
-__global__ __launch_bounds__(256) void k_inverse_perm(const uint32_t *__restrict__ perm, long long n,
-                                                      uint32_t *__restrict__ inv) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i < n) inv[perm[i]] = (uint32_t)i;
 }
 
 // tile_off[nc] and the tile count (the scan is exclusive: add the last cell's count)
@@ -683,11 +597,15 @@ __device__ unsigned long long g_dbg_t[8192][16];
 __device__ unsigned long long g_dbg_l[65536][4];
 #define DBG_L(k) do { if (threadIdx.x == 0 && blockIdx.x < 65536) g_dbg_l[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 __device__ unsigned long long g_dbg_e[8192][8];
+// k-means++ per-step work counters [centre][eval items, eval reached cells, apply items, apply reached]
+__device__ unsigned long long g_dbg_kpp[4096][4];
+#define DBG_KPP(c, k, v) do { if ((c) < 4096 && (v)) atomicAdd(&g_dbg_kpp[c][k], (unsigned long long)(v)); } while (0)
 #define DBG_E(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_e[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define DBG_EV(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_e[blockIdx.x][k] = (unsigned long long)(v); } while (0)
 #else
 #define DBG_E(k) do { } while (0)
 #define DBG_EV(k, v) do { } while (0)
+#define DBG_KPP(c, k, v) do { } while (0)
 #define DBG_T(k) do { } while (0)
 #define DBG_V(k, v) do { } while (0)
 #define DBG_L(k) do { } while (0)

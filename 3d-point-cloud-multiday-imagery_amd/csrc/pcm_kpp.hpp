@@ -8,8 +8,8 @@
 // (in the caller's row order), targets floor(u * pot) computed exactly from u's
 // 53-bit mantissa.
 //
-// The cloud is laid out in pruning-grid cell order (the Lloyd engine's
-// k_cellid / radix sort / AoSoA-4 gather).  Per centre c = 1 .. k-1, three
+// The cloud is laid out in pruning-grid cell order (the Lloyd engine's record
+// sort, pcm_sort.hpp: AoSoA-4 points + perm).  Per centre c = 1 .. k-1, three
 // stream-ordered launches:
 //   k_kpp_search  L blocks: target t's original-order weight block by an exact
 //                 prefix over the block sums `bsum`, then the first row of that
@@ -467,6 +467,10 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
                     if (kpp_reaches<D>(g, cl, s_cand[q], cm)) lmask |= 1u << q;
             }
             unsigned long long bits = __ballot(lmask != 0u);
+            if (lane == 0) {
+                DBG_KPP(c, 0, (unsigned)min(64LL, cpw - k0));
+                DBG_KPP(c, 1, __popcll(bits));
+            }
             while (bits) {
                 const int src = __builtin_ctzll(bits);
                 bits &= bits - 1ull;
@@ -508,6 +512,10 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
             }
             unsigned long long bits = __ballot(reach);
             dbg_cells += (unsigned)__popcll(bits);
+            if (lane == 0) {
+                DBG_KPP(c, 0, (unsigned)min(64LL, ipw - k0));
+                DBG_KPP(c, 1, __popcll(bits));
+            }
             while (bits) {
                 const int src = __builtin_ctzll(bits);
                 bits &= bits - 1ull;
@@ -589,6 +597,10 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
             reach = kpp_reaches<D>(g, celll, best, cm);
         }
         unsigned long long bits = __ballot(reach);
+        if (lane == 0) {
+            DBG_KPP(c, 2, (unsigned)min(64LL, ipw - k0));
+            DBG_KPP(c, 3, __popcll(bits));
+        }
         while (bits) {
             const int src = __builtin_ctzll(bits);
             bits &= bits - 1ull;
