@@ -40,14 +40,32 @@ constexpr int KPP_CELL_PTS = 256;              // target points per pruning cell
 constexpr int KPP_STPB = 1024;                 // k_kpp_search block size
 constexpr int KPP_RED_BLOCKS = 64;             // gmax reduction blocks of k_kpp_search
 constexpr int KPP_SCU = 32;                    // k_kpp_search: 64-wide chunks of block sums kept in registers per wave
+// Same-address device atomics serialise at the memory side (~12 ns each,
+// MI355X_MICROARCH.md "fanin") and stall the loads queued behind them: 1024
+// per-wave atomicMax on one gmax word held k_kpp_search's block-sum loads for
+// ~10 us, thousands of per-wave adds on the 8 candidate potentials held
+// k_kpp_eval's cell loads.  Reductions therefore go through LDS, then per-block
+// plain stores (gmax) or adds spread over KPP_DREP replica lines (potentials).
+constexpr int KPP_DREP = 32;
 
 struct KppCtl {
     float4 cand[KPP_LMAX];
     long long cand_idx[KPP_LMAX];
     unsigned long long pot[2];                 // potential at the start of step c: pot[c & 1]
-    unsigned long long delta[KPP_LMAX];        // potential drop of each candidate (k_kpp_eval)
-    unsigned int gmax_acc[2];                  // float bits: max closest, reduced by step c's search into [c & 1]
+    unsigned long long drep[KPP_DREP][KPP_LMAX];   // potential drop of each candidate: sum of the replicas (k_kpp_eval)
+    unsigned int gpart[KPP_RED_BLOCKS];        // float bits: max closest per reduction block of step c's search
 };
+
+// gmax = max of the reduction blocks' parts (whole block must call)
+__device__ __forceinline__ float kpp_gmax(const KppCtl *__restrict__ ctl, unsigned *s_g) {
+    if (threadIdx.x < 64) {
+        unsigned m = threadIdx.x < KPP_RED_BLOCKS ? ctl->gpart[threadIdx.x] : 0u;
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+        if (threadIdx.x == 0) *s_g = m;
+    }
+    __syncthreads();
+    return __uint_as_float(*s_g);
+}
 
 // w = trunc(ldexp(double(d), s)) for d >= 0, from the fp32 fields with integer
 // ops (exact: d = mant * 2^e2 before scaling; w < 2^64 by the choice of s).
@@ -286,20 +304,26 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
                                                          long long ncells, KppCtl *__restrict__ ctl) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     DBG_T(0);
-    if ((int)blockIdx.x >= L) {   // gmax: max over the cells' max closest
+    constexpr int NWV = KPP_STPB / 64;
+    if ((int)blockIdx.x >= L) {   // gmax part: max over a slice of the cells' max closest
+        __shared__ unsigned int s_m[NWV];
         unsigned int m = 0u;
         for (long long cl = (blockIdx.x - L) * (long long)KPP_STPB + tid; cl < ncells;
              cl += (long long)(gridDim.x - L) * KPP_STPB)
             m = max(m, __float_as_uint(cmax[cl]));
         for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o));
-        if (lane == 0 && m) atomicMax(&ctl->gmax_acc[c & 1], m);
+        if (lane == 0) s_m[wv] = m;
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < NWV; ++w) m = max(m, s_m[w]);
+            ctl->gpart[blockIdx.x - L] = m;
+        }
         DBG_T(8);
         return;
     }
     const int t = blockIdx.x;
     if (t == 0)
-        for (int l = tid; l < KPP_LMAX; l += KPP_STPB) ctl->delta[l] = 0ull;
-    constexpr int NWV = KPP_STPB / 64;
+        for (int l = tid; l < KPP_DREP * KPP_LMAX; l += KPP_STPB) (&ctl->drep[0][0])[l] = 0ull;
     __shared__ unsigned long long wtot[NWV];
     __shared__ long long s_blk;
     __shared__ unsigned long long s_res;
@@ -422,11 +446,13 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
     __shared__ int s_i0[KPP_LMAX][MAXD], s_i1[KPP_LMAX][MAXD];
     __shared__ long long s_off[KPP_LMAX + 1];
     __shared__ float4 s_cand[KPP_LMAX];
-    const int tid = threadIdx.x, lane = tid & 63;
+    __shared__ unsigned s_g;
+    __shared__ unsigned long long s_red[4][KPP_LMAX];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     DBG_E(0);
-    const float gmax = __uint_as_float(ctl->gmax_acc[c & 1]);
+    const float4 cd = ctl->cand[tid < L ? tid : 0];   // issued together with the gmax parts
+    const float gmax = kpp_gmax(ctl, &s_g);
     if (tid < L) {
-        const float4 cd = ctl->cand[tid];
         int i0[MAXD], i1[MAXD];
         long long vol;
         kpp_cube<D>(g, cd, gmax, i0, i1, vol);
@@ -511,6 +537,7 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
                 reach = kpp_reaches<D>(g, cell, s_cand[l], cm);
             }
             unsigned long long bits = __ballot(reach);
+            if (k0 == 0) DBG_E(3);
             dbg_cells += (unsigned)__popcll(bits);
             if (lane == 0) {
                 DBG_KPP(c, 0, (unsigned)min(64LL, ipw - k0));
@@ -530,6 +557,7 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
 #pragma unroll
                 for (int q = 0; q < KPP_LMAX; ++q)
                     if (q == lq) dw[q] += v;
+                if (dbg_cells > 0u && k0 == 0) DBG_E(6);
             }
         }
     }
@@ -542,13 +570,22 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
     unsigned long long nz = 0ull;
 #pragma unroll
     for (int q = 0; q < KPP_LMAX; ++q) nz |= dw[q];
-    if (__ballot(nz != 0ull) == 0ull) return;   // wave-uniform
+    if (__ballot(nz != 0ull) != 0ull) {   // wave-uniform
 #pragma unroll
-    for (int q = 0; q < KPP_LMAX; ++q) {
-        if (q >= L) break;
-        const unsigned long long v = wave_sum_u64(dw[q]);
-        if (lane == 0 && v) atomicAdd(&ctl->delta[q], v);
+        for (int q = 0; q < KPP_LMAX; ++q) {
+            if (q >= L) break;
+            const unsigned long long v = wave_sum_u64(dw[q]);
+            if (lane == 0) s_red[wv][q] = v;
+        }
+    } else if (lane < KPP_LMAX) {
+        s_red[wv][lane] = 0ull;
     }
+    __syncthreads();
+    if (tid < L) {
+        const unsigned long long v = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
+        if (v) atomicAdd(&ctl->drep[blockIdx.x % KPP_DREP][tid], v);
+    }
+    DBG_E(7);
 }
 
 // Step c: select (first argmin of the candidates' potentials) and, unless this
@@ -560,20 +597,30 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
                                                    float *__restrict__ cmax, unsigned long long *__restrict__ bsum,
                                                    int L, int s, int c, int apply, long long *__restrict__ indices,
                                                    KppCtl *__restrict__ ctl) {
+    __shared__ unsigned s_g;
+    __shared__ unsigned long long s_del[KPP_LMAX];
     const int tid = threadIdx.x, lane = tid & 63;
     const unsigned long long pot = ctl->pot[c & 1];
+    if (tid < L) {   // candidate tid's potential drop: the sum of the replicas
+        unsigned long long v[KPP_DREP];
+#pragma unroll
+        for (int r = 0; r < KPP_DREP; ++r) v[r] = ctl->drep[r][tid];
+        unsigned long long sum = 0ull;
+#pragma unroll
+        for (int r = 0; r < KPP_DREP; ++r) sum += v[r];
+        s_del[tid] = sum;
+    }
+    const float gmax = kpp_gmax(ctl, &s_g);   // (its barrier publishes s_del)
     int bl = 0;
-    unsigned long long bp = pot - ctl->delta[0];
+    unsigned long long bp = pot - s_del[0];
     for (int q = 1; q < L; ++q) {
-        const unsigned long long v = pot - ctl->delta[q];
+        const unsigned long long v = pot - s_del[q];
         if (v < bp) { bp = v; bl = q; }   // first argmin (np.argmin)
     }
     const float4 best = ctl->cand[bl];
-    const float gmax = __uint_as_float(ctl->gmax_acc[c & 1]);
     if (blockIdx.x == 0 && tid == 0) {
         indices[c] = ctl->cand_idx[bl];
         ctl->pot[(c + 1) & 1] = bp;
-        ctl->gmax_acc[(c + 1) & 1] = 0u;
     }
     if (!apply) return;
     int i0[MAXD], i1[MAXD];

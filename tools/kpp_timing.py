@@ -40,6 +40,8 @@ e = e[e[:, 0] >= e[:, 0].max() - 30000]
 nb = len(e)
 t0 = e[:, 0].min()
 print(f"eval blocks {nb}: items total {int(e[0, 5])}; reached cells of wave 0 p50 {np.median(e[:, 4]):.0f} max {e[:, 4].max()}")
-for k, name in ((0, "start"), (1, "setup"), (2, "cells done")):
-    v = (e[:, k] - t0) / 100.0
+for k, name in ((0, "start"), (1, "setup"), (3, "reach tests"), (6, "first cell"), (2, "cells done"), (7, "end")):
+    if not (e[:, k] > 0).any():
+        continue
+    v = (e[e[:, k] > 0, k] - t0) / 100.0
     print(f"  {name:10s} us after first start: p50 {np.median(v):6.2f} p90 {np.percentile(v, 90):6.2f} max {v.max():6.2f}")

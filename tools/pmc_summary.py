@@ -7,6 +7,7 @@ usage: python tools/pmc_summary.py KERNEL_SUBSTR DIR [DIR ...]
 """
 import csv
 import glob
+import os
 import json
 import sqlite3
 import sys
@@ -41,7 +42,9 @@ def main():
         dbs = glob.glob(f"{d}/**/*.db", recursive=True)
         per = load_db(dbs[0], kernel) if dbs else load_csv(glob.glob(f"{d}/**/*counter_collection.csv",
                                                                       recursive=True), kernel)
-        for i in sorted(per)[1:]:
+        ids = sorted(per)[1:]
+        last = int(os.environ.get("PMC_LAST", "0"))   # only the last N dispatches (e.g. late k-means++ steps)
+        for i in (ids[-last:] if last > 0 else ids):
             for k, v in per[i].items():
                 agg[k].append(v)
     out = {k: sum(v) / len(v) for k, v in agg.items()}
