@@ -415,7 +415,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->cand_stats, 3 * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->empty_idx, (size_t)k * sizeof(int));
     err = err ? err : hipMalloc(&e->ntiles_dev, 2 * sizeof(uint32_t));
-    err = err ? err : hipMalloc(&e->zpts, sizeof(unsigned long long));
+    err = err ? err : hipMalloc(&e->zpts, 32 * 16 * sizeof(unsigned long long));
     err = err ? err : hipMemset(e->partials, 0, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMemset(e->ctrl, 0, sizeof(Ctrl));
     if (err != hipSuccess) {
@@ -679,7 +679,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     // compressed point stream for k_lloyd1 (fp32, D = 3; PCM_XZ=0 disables it: A/B measurement only)
     static const bool xz_on = [] { const char *v = std::getenv("PCM_XZ"); return !(v && std::atoi(v) == 0); }();
     e->use_xz = xz_on && e->dtype == PCM_F32 && e->d == 3;
-    HIPCHK(hipMemsetAsync(e->zpts, 0, sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(e->zpts, 0, 32 * 16 * sizeof(unsigned long long), s));
     if (e->use_xz) {
         HIPCHK(ensure(e->xz, e->cap_xz, (size_t)e->npad * 8));
         HIPCHK(ensure(e->tmeta, e->cap_tmeta, (size_t)e->ntiles_cap * sizeof(uint4)));
@@ -840,8 +840,14 @@ static int launch_labels(pcm_engine *e, hipStream_t s, unsigned long long *inert
         if (e->n == 0) return 0;
         return dispatch_l(e, [&](auto L) -> int {
             using LT = decltype(L);
-            k_label<TT, D, LT><<<assign_grid(e, (const void *)k_label<TT, D, LT>, 0), TPB, 0, s>>>(A, e->lab, inert, e->iscale);
+            // inertia limbs: per-block replica lines, folded into inert[] afterwards
+            unsigned long long *rep = inert ? &e->ctrl->inert_rep[0][0] : nullptr;
+            k_label<TT, D, LT><<<assign_grid(e, (const void *)k_label<TT, D, LT>, 0), TPB, 0, s>>>(A, e->lab, rep, e->iscale);
             LAUNCHCHK();
+            if (inert) {
+                k_inert_fold<<<1, 64, 0, s>>>(rep, inert);
+                LAUNCHCHK();
+            }
             return 0;
         });
     });
@@ -1202,8 +1208,9 @@ int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid) 
 int pcm_layout_stream_bytes(pcm_engine *e, double *bytes, int64_t *compressed_points) {
     if (!e || !bytes || !compressed_points) return fail(PCM_E_ARG, "bad argument");
     if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
-    unsigned long long z = 0;
-    HIPCHK(hipMemcpy(&z, e->zpts, sizeof(z), hipMemcpyDeviceToHost));
+    unsigned long long zr[32 * 16], z = 0;   // replica lines of k_tile_compress
+    HIPCHK(hipMemcpy(zr, e->zpts, sizeof(zr), hipMemcpyDeviceToHost));
+    for (int r = 0; r < 32; ++r) z += zr[r * 16];
     const double raw = (double)e->d * (double)tsize(e->dtype);
     *compressed_points = (int64_t)z;
     *bytes = (double)z * 8.0 + (double)(e->n - (long long)z) * raw;

@@ -53,6 +53,7 @@ struct Grid {
 };
 
 // Device control block (one per engine).
+constexpr int INERT_REP = 32;
 struct Ctrl {
     uint32_t halt, done, iter, max_iter;
     uint32_t n_empty, resume, status, pad0;
@@ -67,6 +68,12 @@ struct Ctrl {
     unsigned int rebuilds;          // candidate-list rebuilds of this fit (diagnostics)
     unsigned int pad1;
     unsigned long long neq_acc;     // k_step: changed statistic words, summed over blocks (last arriver reads, resets)
+    // k_step's ~512 blocks arrive spread over ~20 us: one counter line measured as fast as two levels
+    // over 8 group lines (24.8-26 vs 27.3 us per launch), so the arrival stays single-level.
+    // Same-address device atomics serialise at the memory side (~12 ns each, MI355X_MICROARCH.md
+    // "fanin") and hold back loads queued behind them, so bulk per-wave adds are spread instead:
+    // k_label: exact-inertia limbs added per block into replica lines (folded by k_inert_fold)
+    alignas(128) unsigned long long inert_rep[INERT_REP][16];
 };
 
 // Fixed-point exponents q_a (identical on every rank).
@@ -383,7 +390,7 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
         ok = ok && total <= 64u;
         meta = make_uint4(lo[0], lo[1], lo[2], ok ? (0x80000000u | w[0] | (w[1] << 8) | (w[2] << 16)) : 0u);
         tmeta[t] = meta;
-        if (ok) atomicAdd(zpts, (unsigned long long)(end - start));
+        if (ok) atomicAdd(zpts + (t % 32u) * 16u, (unsigned long long)(end - start));   // 32 replica lines
     }
     __syncthreads();
     const uint4 m = meta;
@@ -1268,14 +1275,36 @@ __device__ __forceinline__ void inert_add(unsigned long long &lo, unsigned long 
     hi += (lo < w) ? 1ull : 0ull;
 }
 
+// Block-wide: the limbs of all threads summed, then one add per limb into the
+// block's replica line out[blockIdx % INERT_REP][0..3] (k_inert_fold sums them).
 __device__ __forceinline__ void inert_flush(unsigned long long lo, unsigned long long hi, unsigned ovf,
                                             unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long s_l[TPB / 64][4];
     unsigned long long l[4] = {lo & 0xffffffffull, lo >> 32, hi, (unsigned long long)ovf};
+    const int wv = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         for (int o = 32; o > 0; o >>= 1) l[q] += __shfl_xor(l[q], o);
-        if ((threadIdx.x & 63) == 0 && l[q]) atomicAdd(out + q, l[q]);
+        if ((threadIdx.x & 63) == 0) s_l[wv][q] = l[q];
     }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long v = 0ull;
+        for (int w = 0; w < TPB / 64; ++w) v += s_l[w][threadIdx.x];
+        if (v) atomicAdd(out + (size_t)(blockIdx.x % INERT_REP) * 16 + threadIdx.x, v);
+    }
+}
+
+// inert[0..3] += the replica sums; replicas := 0 (one 64-thread block)
+__global__ void k_inert_fold(unsigned long long *__restrict__ rep, unsigned long long *__restrict__ inert) {
+    const int q = threadIdx.x;
+    if (q >= 4) return;
+    unsigned long long v = 0ull;
+    for (int r = 0; r < INERT_REP; ++r) {
+        v += rep[r * 16 + q];
+        rep[r * 16 + q] = 0ull;
+    }
+    inert[q] += v;
 }
 
 // E-step with the current centres writing labels (sorted order) and the
@@ -2162,6 +2191,8 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
             }
             ctrl->last_changed = changed;
             ctrl->last_shift = shift;
+            ctrl->step_done = 0u;
+            ctrl->neq_acc = 0ull;
             ctrl->resume = 0u;
             uint32_t done = 0;
             if (changed == 0ull) done = 1u;
@@ -2384,8 +2415,6 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
             }
             ctrl->last_changed = changed;
             ctrl->last_shift = shift;
-            ctrl->step_done = 0u;
-            ctrl->neq_acc = 0ull;
             ctrl->resume = 0u;
             if (rebuild) {
                 ctrl->ref_sel = sel ^ 1u;
