@@ -2191,8 +2191,6 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
             }
             ctrl->last_changed = changed;
             ctrl->last_shift = shift;
-            ctrl->step_done = 0u;
-            ctrl->neq_acc = 0ull;
             ctrl->resume = 0u;
             uint32_t done = 0;
             if (changed == 0ull) done = 1u;
@@ -2415,6 +2413,8 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
             }
             ctrl->last_changed = changed;
             ctrl->last_shift = shift;
+            ctrl->step_done = 0u;
+            ctrl->neq_acc = 0ull;
             ctrl->resume = 0u;
             if (rebuild) {
                 ctrl->ref_sel = sel ^ 1u;
