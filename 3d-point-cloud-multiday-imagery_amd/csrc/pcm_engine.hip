@@ -74,6 +74,9 @@ struct pcm_engine {
     uint32_t *zcnt = nullptr;        // occupancy sample counts [ncells + 1]
     size_t cap_tbox = 0, cap_tlc = 0, cap_tlr = 0, cap_tll = 0, cap_zcnt = 0;
     uint32_t *perm = nullptr;
+    uint32_t *dmap = nullptr;        // [2][n] the layout sort's per-pass position maps (labels back to row order)
+    size_t cap_dmap = 0;
+    bool has_dmap = false;           // the current layout kept them (2-pass sorts)
     void *lab = nullptr;             // sorted-order labels: uint16 when k <= 65535, else int32
     uint32_t *cell_start = nullptr;
     uint32_t *sub_start = nullptr;   // [(ncells << d) + 1]: first sorted point of every sub-cell (half-cell per axis)
@@ -193,7 +196,7 @@ void rs_plan(long long n, unsigned bits, RsPlan &p) {
 // and perm (sorted position -> row).
 template <typename TT, int D>
 int rs_sort(const TT *X, long long n, long long npad, const Grid &g, int with_sub, int zlev, unsigned bits,
-            const RsPlan &p, char *wb, TT *xs, uint32_t *perm, hipStream_t s) {
+            const RsPlan &p, char *wb, TT *xs, uint32_t *perm, hipStream_t s, uint32_t *dmaps = nullptr) {
     using R = PRec<TT, D>;
     R *ra = (R *)(wb + p.o_ra), *rb = (R *)(wb + p.o_rb);
     uint32_t *hist = (uint32_t *)(wb + p.o_hist), *goff = (uint32_t *)(wb + p.o_goff),
@@ -215,7 +218,7 @@ int rs_sort(const TT *X, long long n, long long npad, const Grid &g, int with_su
         LAUNCHCHK();
 #define PCM_RS_SCATTER(FX, TX)                                                                                      \
     k_rs_scatter<TT, D, FX, TX><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, goff, segb, rout, \
-                                                        xs, perm)
+                                                        xs, perm, dmaps ? dmaps + (size_t)q * n : nullptr)
         if (from_x && to_xs) PCM_RS_SCATTER(true, true);
         else if (from_x) PCM_RS_SCATTER(true, false);
         else if (to_xs) PCM_RS_SCATTER(false, true);
@@ -235,13 +238,15 @@ int rs_sort(const TT *X, long long n, long long npad, const Grid &g, int with_su
 void free_layout(pcm_engine *e) {
     e->layout_ready = false;
     e->fit_ready = false;
+    e->has_dmap = false;
 }
 
 void free_buffers(pcm_engine *e) {
     void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->ws,
-                  e->sub_start, e->xz, e->tmeta, e->tbox, e->tl_cnt, e->tl_rec, e->tl_lab, e->zcnt};
+                  e->sub_start, e->xz, e->tmeta, e->tbox, e->tl_cnt, e->tl_rec, e->tl_lab, e->zcnt, e->dmap};
     for (void *p : ps)
         if (p) (void)hipFree(p);
+    e->dmap = nullptr; e->cap_dmap = 0; e->has_dmap = false;
     e->xs = nullptr; e->perm = nullptr; e->lab = nullptr; e->cell_start = nullptr; e->tiles = nullptr;
     e->tile_off = nullptr; e->ws = nullptr; e->sub_start = nullptr; e->cap_sub = 0;
     e->xz = nullptr; e->tmeta = nullptr; e->cap_xz = e->cap_tmeta = 0; e->use_xz = false;
@@ -649,8 +654,10 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         char *wb = (char *)e->ws;
         tcnt = (uint32_t *)(wb + o_tcnt);
         tmp = wb + o_tmp;
+        // 2-pass sorts keep their position maps for pcm_labels
+        e->has_dmap = p.npass == 2 && ensure(e->dmap, e->cap_dmap, (size_t)2 * n * sizeof(uint32_t)) == hipSuccess;
         if (int rc2 = rs_sort<TT, D>((const TT *)X, n, e->npad, e->g, e->sub, e->zlev, bits, p, wb, (TT *)e->xs,
-                                     e->perm, s))
+                                     e->perm, s, e->has_dmap ? e->dmap : nullptr))
             return rc2;
         // cell (or sub-cell) starts by binary search over the sorted points
         if (e->zlev > 0)   // Morton-ordered cells: the keys' cell bits
@@ -1116,12 +1123,24 @@ int pcm_labels(pcm_engine *e, int32_t *out, void *stream) {
     // int32 -- 100M points: 1.52 vs 2.11 ms for the direct int32 scatter
     // (tools/unperm_sweep.sh; windows of 64M/32M rows: 1.88/1.93 ms).
     // PCM_UNPERM / PCM_UNPERM_WIN: tuning sweeps only.
-    static const int mode = [] { const char *v = std::getenv("PCM_UNPERM"); return v ? std::atoi(v) : 1; }();
+    static const int mode = [] { const char *v = std::getenv("PCM_UNPERM"); return v ? std::atoi(v) : 3; }();
     static const long long win = [] { const char *v = std::getenv("PCM_UNPERM_WIN"); return v ? std::atoll(v) : (1LL << 40); }();
     return dispatch_l(e, [&](auto L) -> int {
         using LT = decltype(L);
         const bool a16 = ((uintptr_t)out & 15u) == 0;
-        if (mode == 1 && std::is_same<LT, uint16_t>::value && a16) {
+        if (mode == 3 && e->has_dmap) {
+            // the sort's two position maps, inverted by two run-wise gathers:
+            // sorted -> between the passes -> caller rows
+            if (ensure(e->ws, e->cap_ws, (size_t)e->n * sizeof(LT) + 64) != hipSuccess)
+                return fail(PCM_E_NOMEM, "labels scratch");
+            LT *mid = (LT *)e->ws;
+            k_lab_gather<LT><<<blocks_for(e->n), 256, 0, s>>>(e->dmap + e->n, (const LT *)e->lab, e->n, mid);
+            LAUNCHCHK();
+            k_lab_gather_i32<LT><<<blocks_for(e->n), 256, 0, s>>>(e->dmap, mid, e->n, out);
+            LAUNCHCHK();
+            return 0;
+        }
+        if (mode >= 1 && std::is_same<LT, uint16_t>::value && a16) {
             // uint16 scatter into scratch (n * 2 B), in destination windows, then a sequential widen
             if (ensure(e->ws, e->cap_ws, (size_t)e->n * 2 + 64) != hipSuccess) return fail(PCM_E_NOMEM, "labels scratch");
             uint16_t *t16 = (uint16_t *)e->ws;

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_scatter(const T *__restrict__ X, 
                                                        const uint32_t *__restrict__ goff,
                                                        const uint32_t *__restrict__ segb,
                                                        PRec<T, D> *__restrict__ rout, T *__restrict__ xs,
-                                                       uint32_t *__restrict__ perm) {
+                                                       uint32_t *__restrict__ perm, uint32_t *__restrict__ dmap) {
     constexpr int IPT = RsCfg<T, D>::IPT, CH = RsCfg<T, D>::CH, PW = CH / 4;
     __shared__ PRec<T, D> stage[CH];
     __shared__ uint8_t sdig[CH];
@@ -225,6 +225,7 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_scatter(const T *__restrict__ X, 
             const uint32_t p = dstart[d] + wc[wv][d] + (dk[j] >> 8);
             stage[p] = r[j];
             sdig[p] = (uint8_t)d;
+            if (dmap) dmap[i] = (uint32_t)(p + gdelta[d]);   // this pass's input position -> output position
         }
     }
     __syncthreads();
@@ -259,6 +260,24 @@ __global__ __launch_bounds__(256) void k_cell_starts_xs(const T *__restrict__ xs
         if ((long long)(sort_key_f<D>(x, g, with_sub, zlev) >> shift) < c) lo = mid + 1; else hi = mid;
     }
     start[c] = (uint32_t)lo;
+}
+
+// Labels back to the caller's row order through the sort's per-pass position
+// maps (dmap_q: input position of pass q -> its output position), one gather
+// per pass from the last to the first: a pass's outputs are runs of its input
+// order, so the gathers read runs instead of single random words.
+template <typename LT>
+__global__ __launch_bounds__(256) void k_lab_gather(const uint32_t *__restrict__ dmap, const LT *__restrict__ src,
+                                                    long long n, LT *__restrict__ dst) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[dmap[i]];
+}
+
+template <typename LT>
+__global__ __launch_bounds__(256) void k_lab_gather_i32(const uint32_t *__restrict__ dmap, const LT *__restrict__ src,
+                                                        long long n, int32_t *__restrict__ out) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (int32_t)src[dmap[i]];
 }
 
 // xs padding [n, npad): zeros
