@@ -1480,7 +1480,7 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
             LAUNCHCHK();
             k_kpp_eval<D><<<eg, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
             LAUNCHCHK();
-            k_kpp_apply<D><<<eg, 256, 0, s>>>(xs, perm, cell_start, g, closest, crow, cmax, bsum, L, scale, c,
+            k_kpp_apply<D><<<eg, 256, 0, s>>>(xs, perm, cell_start, g, closest, crow, cmax, bsum, X, n, L, scale, c,
                                               c + 1 < k ? 1 : 0, (long long *)indices, ctl);
             LAUNCHCHK();
         }

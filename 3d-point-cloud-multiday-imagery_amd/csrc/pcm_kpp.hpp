@@ -595,9 +595,11 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
                                                    const uint32_t *__restrict__ cell_start, Grid g,
                                                    float *__restrict__ closest, float *__restrict__ crow,
                                                    float *__restrict__ cmax, unsigned long long *__restrict__ bsum,
+                                                   const float *__restrict__ X, long long n,
                                                    int L, int s, int c, int apply, long long *__restrict__ indices,
                                                    KppCtl *__restrict__ ctl) {
     __shared__ unsigned s_g;
+    __shared__ unsigned long long s_w[4];
     __shared__ unsigned long long s_del[KPP_LMAX];
     const int tid = threadIdx.x, lane = tid & 63;
     const unsigned long long pot = ctl->pot[c & 1];
@@ -626,6 +628,12 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
     int i0[MAXD], i1[MAXD];
     long long vol;
     kpp_cube<D>(g, best, gmax, i0, i1, vol);
+    // Dense step (the cube covers >= 7/8 of the grid: the first ~10-20
+    // centres): the caller-order copy `crow` and the block sums are rebuilt by a
+    // streaming pass over the caller's rows at the end of this launch instead
+    // of one random 4-B write and one random atomic per updated point (every
+    // point outside the cube keeps its value: its distance exceeds gmax).
+    const bool dense = 8 * vol >= 7 * g.ncells;
     const long long wid = (blockIdx.x * (long long)blockDim.x + tid) >> 6;
     const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
     // this wave's cube cells wid, wid + nw, ...: reach tests one per lane (one
@@ -657,16 +665,44 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
             kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t i, const float (&x)[D], float cl) {
                 const float d = dist_canon<D>(x, best);
                 if (d < cl) {
-                    const uint32_t r = perm[i];
                     closest[i] = d;
-                    crow[r] = d;
-                    atomicAdd(&bsum[r >> KPP_OB_LOG], ~(kpp_w(cl, s) - kpp_w(d, s)) + 1ull);   // -= (mod 2^64)
+                    if (!dense) {
+                        const uint32_t r = perm[i];
+                        crow[r] = d;
+                        atomicAdd(&bsum[r >> KPP_OB_LOG], ~(kpp_w(cl, s) - kpp_w(d, s)) + 1ull);   // -= (mod 2^64)
+                    }
                 }
                 mx = fmaxf(mx, fminf(d, cl));
             });
             mx = wave_max_f(mx);
             if (lane == 0) cmax[cell] = mx;
         }
+    }
+    if (!dense) return;
+    // rows: crow[j] = min(crow[j], d(X_j, best)), bsum[b] = its block's weight sum
+    const long long nb = (n + KPP_OB - 1) / KPP_OB;
+    const int wv = tid >> 6;
+    for (long long b = blockIdx.x; b < nb; b += gridDim.x) {
+        unsigned long long acc = 0ull;
+#pragma unroll 4
+        for (int e = 0; e < KPP_OB / 256; ++e) {
+            const long long j = b * KPP_OB + e * 256 + tid;
+            if (j < n) {
+                float x[D];
+#pragma unroll
+                for (int a = 0; a < D; ++a) x[a] = X[j * D + a];
+                const float cl = crow[j];
+                const float d = dist_canon<D>(x, best);
+                const float m = d < cl ? d : cl;
+                if (d < cl) crow[j] = d;
+                acc += kpp_w(m, s);
+            }
+        }
+        acc = wave_sum_u64(acc);
+        if (lane == 0) s_w[wv] = acc;
+        __syncthreads();
+        if (tid == 0) bsum[b] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
     }
 }
 
