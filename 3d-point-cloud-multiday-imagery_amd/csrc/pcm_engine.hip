@@ -752,10 +752,15 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
 // (sharded) clouds; D = 4 coarse cells hold 256 fine cells.
 // Measured (round-2 bpc sweep, tools/sweep.sh PCM_CAND_BPC_RT): 12.5M-point shard (64 coarse cells) 8 -> 39 us
 // vs 4 -> 47 us per update; 100M (512 coarse cells) 1; D = 4, K = 4096: 32.
+// Fine grids (short lists, the 8-slot k_lloyd1: an 8-way slab, 64 coarse cells)
+// want about one block per CU (round-3 slab sweep, profiles/r3x_slab_sweep.txt:
+// bpc 4 -> 18.6 us, 2 -> 19.2, 8 -> 21.0, 16 -> 31.2 per update).
+static int lloyd_slots(const pcm_engine *e);
 static int cand_bpc(const pcm_engine *e) {
     if (const char *ov = std::getenv("PCM_CAND_BPC_RT")) return std::max(1, std::atoi(ov));   // tuning sweeps only
     if (e->d >= 4) return 32;
-    long long b = (2LL * e->num_cu + e->g.ncoarse - 1) / std::max(1LL, e->g.ncoarse);
+    const long long per = (lloyd_slots(e) == 8 ? 1LL : 2LL) * e->num_cu;
+    long long b = (per + e->g.ncoarse - 1) / std::max(1LL, e->g.ncoarse);
     return (int)std::max(1LL, std::min(8LL, b));
 }
 

@@ -23,8 +23,12 @@
 
 namespace pcm {
 
-constexpr int RS_TPB = 256;
-constexpr int RS_DIG = 256;   // digit values per pass (<= 8 bits)
+#ifndef PCM_RS_TPB
+#define PCM_RS_TPB 256
+#endif
+constexpr int RS_TPB = PCM_RS_TPB;   // threads per sort block (256 or 512)
+constexpr int RS_NWV = RS_TPB / 64;
+constexpr int RS_DIG = 256;          // digit values per pass (<= 8 bits)
 
 template <typename T, int D> struct RsCfg {
     // items per thread: the LDS staging of a chunk (record + digit per item) <= 68 KB.  Longer
@@ -66,9 +70,9 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_count(const T *__restrict__ X, co
                                                      long long n, Grid g, int with_sub, int zlev, int shift, int width,
                                                      uint32_t *__restrict__ hist) {
     constexpr int IPT = RsCfg<T, D>::IPT, CH = RsCfg<T, D>::CH;
-    __shared__ uint32_t h[4][RS_DIG];
+    __shared__ uint32_t h[RS_NWV][RS_DIG];
     const int tid = threadIdx.x, wv = tid >> 6;
-    for (int k = tid; k < 4 * RS_DIG; k += RS_TPB) (&h[0][0])[k] = 0u;
+    for (int k = tid; k < RS_NWV * RS_DIG; k += RS_TPB) (&h[0][0])[k] = 0u;
     __syncthreads();
     const long long base = (long long)blockIdx.x * CH;
     const uint32_t mask = (1u << width) - 1u;
@@ -84,8 +88,12 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_count(const T *__restrict__ X, co
         if (i < n) atomicAdd(&h[wv][(rs_key<T, D>(r[j], g, with_sub, zlev) >> shift) & mask], 1u);
     }
     __syncthreads();
-    const uint32_t t = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
-    hist[(long long)blockIdx.x * RS_DIG + tid] = t;   // chunk-major: one coalesced 1-KB row per chunk
+    if (tid < RS_DIG) {
+        uint32_t t = 0u;
+#pragma unroll
+        for (int w = 0; w < RS_NWV; ++w) t += h[w][tid];
+        hist[(long long)blockIdx.x * RS_DIG + tid] = t;   // chunk-major: one coalesced 1-KB row per chunk
+    }
 }
 
 // Output bases, chunk-major like hist: goff[chunk][d] (exclusive over the
@@ -155,15 +163,15 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_scatter(const T *__restrict__ X, 
                                                        const uint32_t *__restrict__ segb,
                                                        PRec<T, D> *__restrict__ rout, T *__restrict__ xs,
                                                        uint32_t *__restrict__ perm, uint32_t *__restrict__ dmap) {
-    constexpr int IPT = RsCfg<T, D>::IPT, CH = RsCfg<T, D>::CH, PW = CH / 4;
+    constexpr int IPT = RsCfg<T, D>::IPT, CH = RsCfg<T, D>::CH, PW = CH / RS_NWV;
     __shared__ PRec<T, D> stage[CH];
     __shared__ uint8_t sdig[CH];
-    __shared__ uint32_t wc[4][RS_DIG];
+    __shared__ uint32_t wc[RS_NWV][RS_DIG];
     __shared__ uint32_t dstart[RS_DIG];
     __shared__ long long gdelta[RS_DIG];
     __shared__ uint32_t wtot[4];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int k = tid; k < 4 * RS_DIG; k += RS_TPB) (&wc[0][0])[k] = 0u;
+    for (int k = tid; k < RS_NWV * RS_DIG; k += RS_TPB) (&wc[0][0])[k] = 0u;
     const long long base = (long long)blockIdx.x * CH;
     const uint32_t mask = (1u << width) - 1u;
     const unsigned long long lt = (1ull << lane) - 1ull;
@@ -194,27 +202,32 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_scatter(const T *__restrict__ X, 
     }
     __syncthreads();
     {
-        // digit tid: offsets of the waves' runs, the chunk's digit starts, output bases
-        const uint32_t c0 = wc[0][tid], c1 = wc[1][tid], c2 = wc[2][tid], c3 = wc[3][tid];
-        const uint32_t tot = c0 + c1 + c2 + c3;
-        wc[0][tid] = 0u;
-        wc[1][tid] = c0;
-        wc[2][tid] = c0 + c1;
-        wc[3][tid] = c0 + c1 + c2;
-        uint32_t v = tot;
+        // digit tid (< RS_DIG): offsets of the waves' runs, the chunk's digit starts, output bases
+        uint32_t tot = 0u, v = 0u;
+        if (tid < RS_DIG) {
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = (uint32_t)__shfl_up((int)v, o);
-            if (lane >= o) v += u;
+            for (int w = 0; w < RS_NWV; ++w) {
+                const uint32_t cw = wc[w][tid];
+                wc[w][tid] = tot;
+                tot += cw;
+            }
+            v = tot;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = (uint32_t)__shfl_up((int)v, o);
+                if (lane >= o) v += u;
+            }
+            if (lane == 63) wtot[wv] = v;
         }
-        if (lane == 63) wtot[wv] = v;
         __syncthreads();
-        uint32_t pre = 0u;
-        for (int w = 0; w < wv; ++w) pre += wtot[w];
-        const uint32_t ex = pre + v - tot;
-        dstart[tid] = ex;
-        gdelta[tid] = (long long)goff[(long long)blockIdx.x * RS_DIG + tid] +
-                      (long long)segb[(long long)(blockIdx.x / RS_SEG) * RS_DIG + tid] - (long long)ex;
+        if (tid < RS_DIG) {
+            uint32_t pre = 0u;
+            for (int w = 0; w < wv; ++w) pre += wtot[w];
+            const uint32_t ex = pre + v - tot;
+            dstart[tid] = ex;
+            gdelta[tid] = (long long)goff[(long long)blockIdx.x * RS_DIG + tid] +
+                          (long long)segb[(long long)(blockIdx.x / RS_SEG) * RS_DIG + tid] - (long long)ex;
+        }
     }
     __syncthreads();
 #pragma unroll
