@@ -67,13 +67,18 @@ __global__ __launch_bounds__(256) void k_dense_assign(const T *__restrict__ X, l
                                                       int32_t *__restrict__ labels, T *__restrict__ dist,
                                                       unsigned long long *__restrict__ stats, int lds_stats,
                                                       DenseCtrl *__restrict__ ctrl, int gate,
-                                                      unsigned long long *__restrict__ inert, int iscale) {
+                                                      unsigned long long *__restrict__ inert, int iscale, int lds_c) {
     if (gate && (ctrl->done != 0u)) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-    T *sc = (T *)sm;                                                   // [k * d]
-    unsigned long long *ls = (unsigned long long *)(sm + (((size_t)k * d * sizeof(T) + 15) / 16) * 16);   // [k * (d + 1)]
+    // centres staged in LDS when they fit (k * d * sizeof(T) <= 64 KB), else read
+    // from global memory (L2/L1-resident: every thread scans them in the same order)
+    const size_t cb = lds_c ? (((size_t)k * d * sizeof(T) + 15) / 16) * 16 : 0;
+    T *scl = (T *)sm;
+    const T *sc = lds_c ? scl : C;                                     // [k * d]
+    unsigned long long *ls = (unsigned long long *)(sm + cb);         // [k * (d + 1)]
     const int nstat = k * (d + 1);
-    for (int j = threadIdx.x; j < k * d; j += blockDim.x) sc[j] = C[j];
+    if (lds_c)
+        for (int j = threadIdx.x; j < k * d; j += blockDim.x) scl[j] = C[j];
     if (stats && lds_stats)
         for (int j = threadIdx.x; j < nstat; j += blockDim.x) ls[j] = 0ull;
     __syncthreads();
@@ -494,8 +499,10 @@ int dense_grid(const pcm_dense *e) {
     return (int)std::max(1LL, std::min<long long>((e->n + 255) / 256, (long long)e->num_cu * 4));
 }
 
+bool dense_lds_c(const pcm_dense *e) { return (size_t)e->k * e->d * tsz(e->dtype) <= 64 * 1024; }
+
 size_t dense_lds(const pcm_dense *e, bool with_stats) {
-    const size_t cbytes = (((size_t)e->k * e->d * tsz(e->dtype) + 15) / 16) * 16;
+    const size_t cbytes = dense_lds_c(e) ? (((size_t)e->k * e->d * tsz(e->dtype) + 15) / 16) * 16 : 0;
     const size_t sbytes = (size_t)e->k * (e->d + 1) * 8;
     return cbytes + (with_stats && cbytes + sbytes <= 64 * 1024 ? sbytes : 0);
 }
@@ -510,7 +517,6 @@ int pcm_dense_create(int device, int64_t n, int d, int k, int dtype, int max_ite
     if (k < 1 || n < 1 || k > n) return pcm_fail(PCM_E_ARG, "need 1 <= k <= n");
     if (dtype != PCM_F32 && dtype != PCM_F64) return pcm_fail(PCM_E_ARG, "dtype must be PCM_F32 or PCM_F64");
     if (max_iter < 1) return pcm_fail(PCM_E_ARG, "max_iter must be >= 1");
-    if ((size_t)k * d * tsz(dtype) > 64 * 1024) return pcm_fail(PCM_E_ARG, "k * d too large for LDS staging");
     if (n >= (1LL << 31)) return pcm_fail(PCM_E_ARG, "n must be < 2^31");
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != device) return pcm_fail(PCM_E_STATE, "current HIP device != device");
@@ -594,11 +600,12 @@ int pcm_dense_iterate(pcm_dense *e, int n_iter, void *stream) {
     return dispatch_t(e->dtype, [&](auto TT) -> int {
         using T = decltype(TT);
         const size_t lds = dense_lds(e, true);
-        const int lds_stats = lds > (((size_t)e->k * e->d * sizeof(T) + 15) / 16) * 16 ? 1 : 0;
+        const int lds_stats = lds > dense_lds(e, false) ? 1 : 0;
+        const int lds_c = dense_lds_c(e) ? 1 : 0;
         for (int it = 0; it < n_iter; ++it) {
             k_dense_assign<T><<<dense_grid(e), 256, lds, s>>>((const T *)e->X, e->n, e->d, (const T *)e->C, e->k, e->q,
                                                              e->labels, (T *)e->dist, e->stats, lds_stats, e->ctrl, 1,
-                                                             nullptr, 0);
+                                                             nullptr, 0, lds_c);
             if (hipGetLastError() != hipSuccess) return pcm_fail(PCM_E_HIP, "k_dense_assign launch");
             k_dense_update<T><<<1, 256, 0, s>>>((const T *)e->X, e->n, e->d, (T *)e->C, e->k, e->q, e->labels,
                                                 (const T *)e->dist, e->stats, e->empty_idx, e->picked,
@@ -617,7 +624,7 @@ int pcm_dense_final(pcm_dense *e, void *stream) {
         using T = decltype(TT);
         k_dense_assign<T><<<dense_grid(e), 256, dense_lds(e, false), s>>>(
             (const T *)e->X, e->n, e->d, (const T *)e->C, e->k, e->q, e->labels, nullptr, nullptr, 0, e->ctrl, 0,
-            e->ctrl->inert, e->iscale);
+            e->ctrl->inert, e->iscale, dense_lds_c(e) ? 1 : 0);
         if (hipGetLastError() != hipSuccess) return pcm_fail(PCM_E_HIP, "final assign launch");
         return 0;
     });

@@ -25,9 +25,10 @@ the boundary, which mirror sklearn's own NumPy calls.  Dtypes follow sklearn
 * D > 4, or float64 input the dense engine can take (the reference's
   1500 x 20 float64 call site): the dense engine (``dense.py``), computing in the
   input precision;
-* float64 point clouds (D <= 4) too large for the dense engine -- centres
-  beyond its 64 KB LDS stage (K * D * 8 bytes) or more than 2**26 distance
-  evaluations per iteration (N * K) -- go to the pruned engine in float32 (the
+* float64 point clouds (D <= 4) too large for brute force -- centres beyond
+  the dense engine's 64 KB LDS stage (K * D * 8 bytes; the dense engine itself
+  then reads them from L2) or more than 2**26 distance evaluations per
+  iteration (N * K) -- go to the pruned engine in float32 (the
   boundary cast of the plugin path; its canonical fp32 fit equals sklearn's
   float64 fit on pixel-unit height-map clouds, tests/test_plugin_cloud_golden.py).
 """

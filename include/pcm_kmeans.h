@@ -269,7 +269,7 @@ int pcm_lr_consistency(const double *left_disp, const double *right_disp, int64_
  * float64, computed in that precision), replacing one _kmeans_single_lloyd
  * call (sklearn/cluster/_kmeans.py:623-752) at the reference's KMeans call site
  * members/jasraj/land_use_classification/core.py:227-228 (~1500 x 20 float64).
- * Brute force over all K with the centres staged in LDS (k*d*sizeof <= 64 KB);
+ * Brute force over all K with the centres staged in LDS when k*d*sizeof <= 64 KB (else read from L2);
  * canonical arithmetic of oracle/dense_ref.py; everything on the device, one
  * process (no sharding).  X (device, n*d, row-major) must stay valid and
  * unchanged from pcm_dense_begin to the last call of the fit.  maxabs (host

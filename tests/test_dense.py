@@ -116,7 +116,9 @@ def test_gpu_dense_fit_matches_oracle_float64(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,d,k,dtype,tol", [(600, 8, 6, np.float32, 0.0), (5000, 33, 17, np.float64, 1e-6),
-                                             (3000, 7, 40, np.float32, 0.0), (1, 5, 1, np.float64, 0.0)])
+                                             (3000, 7, 40, np.float32, 0.0), (1, 5, 1, np.float64, 0.0),
+                                             # centres past the 64 KB LDS stage: read from L2
+                                             (6000, 6, 1500, np.float64, 0.0)])
 def test_gpu_dense_fit_random(gpu, n, d, k, dtype, tol):
     torch, pcm = gpu
     from pcm_amd.dense import dense_fit
