@@ -407,7 +407,11 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->cref, (size_t)2 * k * sizeof(float4));
     err = err ? err : hipMalloc(&e->prev, nstat * sizeof(unsigned long long));
+#ifdef PCM_ABL_DOUBLE_FLUSH
+    err = err ? err : hipMalloc(&e->partials, (size_t)3 * k * (d + 1) * sizeof(unsigned long long));
+#else
     err = err ? err : hipMalloc(&e->partials, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
+#endif
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
     e->stats = e->stats_own;
     err = err ? err : hipMalloc(&e->held, nstat * sizeof(unsigned long long));

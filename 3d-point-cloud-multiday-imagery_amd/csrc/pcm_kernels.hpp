@@ -2044,6 +2044,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             if (pi < npairs && sub == 0 && sacc) {
                 const int slot = pi / (D + 1), qq = pi % (D + 1);
                 atomicAdd(prep + (size_t)cid[slot] * (D + 1) + qq, (unsigned long long)sacc);
+#ifdef PCM_ABL_DOUBLE_FLUSH   // calibration build: the flush's atomics issued twice (a third, unused buffer)
+                atomicAdd(A.partials + 2 * A.pstride + (size_t)cid[slot] * (D + 1) + qq, (unsigned long long)sacc);
+#endif
             }
         }
         if (glab)
