@@ -27,7 +27,7 @@ EXPORTS = [
     "pcm_layout_build", "pcm_fit_begin", "pcm_iter_local", "pcm_iter_global", "pcm_iterate", "pcm_stats_ptr",
     "pcm_bind_stats", "pcm_reloc_candidates", "pcm_reloc_apply", "pcm_final", "pcm_labels", "pcm_get_centers",
     "pcm_history", "pcm_read_status", "pcm_layout_info", "pcm_candidate_stats", "pcm_tile_list_stats", "pcm_synth_uniform",
-    "pcm_assign_bruteforce", "pcm_timing", "pcm_timing_read", "pcm_synth_rows", "pcm_kmeanspp", "pcm_cloud_assemble",
+    "pcm_assign_bruteforce", "pcm_timing", "pcm_timing_read", "pcm_time_assign", "pcm_synth_rows", "pcm_kmeanspp", "pcm_cloud_assemble",
     "pcm_inertia_value", "pcm_kmeanspp_workspace",
     "pcm_dense_create", "pcm_dense_destroy", "pcm_dense_begin", "pcm_dense_iterate", "pcm_dense_final",
     "pcm_dense_status", "pcm_dense_outputs", "pcm_dense_kmeanspp_workspace", "pcm_dense_kmeanspp",
@@ -91,6 +91,7 @@ def _declare(lib):
         "pcm_reloc_apply": ([P, P, I, P], I),
         "pcm_final": ([P, P], I),
         "pcm_labels": ([P, P, P], I),
+        "pcm_time_assign": ([P, I, P, ctypes.POINTER(D)], I),
         "pcm_get_centers": ([P, P, P], I),
         "pcm_history": ([P, P, P, I, P], I),
         "pcm_read_status": ([P, ctypes.POINTER(PcmStatus), P], I),

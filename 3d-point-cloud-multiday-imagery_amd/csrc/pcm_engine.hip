@@ -1021,6 +1021,36 @@ int pcm_timing_read(pcm_engine *e, double *ms, int *count) {
     return 0;
 }
 
+// Calibration of the assign kernel's launch duration: `reps` back-to-back
+// launches on the current layout, lists and centres between ONE HIP event pair
+// (no per-launch events, no k_step between them).  The statistics they add are
+// discarded: the fit must restart with pcm_fit_begin.
+int pcm_time_assign(pcm_engine *e, int reps, void *stream, double *ms) {
+    if (!e || !ms || reps < 1) return fail(PCM_E_ARG, "bad argument");
+    if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
+    hipStream_t s = (hipStream_t)stream;
+    if (int rc = timing_drain(e, true)) return rc;
+    const bool was = e->timing;
+    e->timing = false;
+    hipEvent_t a = nullptr, b = nullptr;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    int rc = 0;
+    HIPCHK(hipEventRecord(a, s));
+    for (int i = 0; i < reps && !rc; ++i) rc = iter_local_impl(e, s, false);
+    HIPCHK(hipEventRecord(b, s));
+    HIPCHK(hipEventSynchronize(b));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    e->timing = was;
+    e->fit_ready = false;   // the partial statistics now hold extra sums
+    if (rc) return rc;
+    *ms = (double)t / reps;
+    return 0;
+}
+
 // Single-process iterations: the fold is fused into k_global (3 launches per iteration).
 int pcm_iterate(pcm_engine *e, int n, void *stream) {
     if (!e || n < 0) return fail(PCM_E_ARG, "bad argument");

@@ -176,6 +176,12 @@ class Engine:
     def timing(self, enable: bool):
         _lib.check(self.lib.pcm_timing(self.h, int(bool(enable))), "pcm_timing")
 
+    def time_assign(self, reps: int) -> float:
+        """Mean ms of `reps` back-to-back assign launches (calibration; the fit must begin again)."""
+        ms = ctypes.c_double()
+        _lib.check(self.lib.pcm_time_assign(self.h, int(reps), _stream(), ctypes.byref(ms)), "pcm_time_assign")
+        return ms.value
+
     def timing_read(self) -> dict:
         ms = np.zeros(3)
         cnt = ctypes.c_int()

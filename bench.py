@@ -474,6 +474,16 @@ def main():
         dt, assign_ms = float(t[0]), float(t[1])
     else:
         assign_ms = tm["assign_ms"]
+    launch_ms, b2b_ms = assign_ms, None
+    if world == 1 and not args.no_events:
+        # reported beside the roofline, not used by it: ONE HIP event pair around
+        # `steps` back-to-back assign launches on the final layout, lists and centres
+        # (no per-launch events, no k_step between them; the statistics they add are
+        # discarded -- nothing iterates this engine afterwards).  They run ~10 % faster
+        # than the same kernel inside the timed replay (rocprof, profiles/r4g_*): the
+        # final lists are built with smaller drift margins, and no k_step runs between,
+        # so the roofline keeps the eager-pass events, the closest to the timed region.
+        b2b_ms = eng.time_assign(args.steps)
 
     fit = kpp_ms = None
     if args.fit_iters > 0 and world == 1:
@@ -516,7 +526,7 @@ def main():
         sb = eng.stream_bytes()
         stream_bytes = sb["bytes"]
         bytes_pt = D * (2 if pdt == torch.float16 else 4)
-        achieved = bytes_pt * n_local / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0
+        achieved = bytes_pt * n_local / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
         traffic, traffic_src = pmc_traffic(N, K, D, world)
         value = N * args.steps / dt
         out = {
@@ -547,8 +557,9 @@ def main():
                          "kernel": eng.assign_kernel(),
                          "algorithmic_bytes_per_point": bytes_pt,
                          "stream_bytes_per_launch": stream_bytes, "compressed_points": sb["compressed_points"],
-                         "stream_GBps": stream_bytes / (assign_ms * 1e-3) / 1e9 if assign_ms > 0 else 0.0,
-                         "avg_launch_ms": assign_ms, "timing": timing + ("" if world == 1 else " (max over ranks)")},
+                         "stream_GBps": stream_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0,
+                         "avg_launch_ms": launch_ms, "avg_launch_ms_back_to_back": b2b_ms,
+                         "timing": timing + ("" if world == 1 else " (max over ranks)")},
             "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"],
                                       "tile_lists": tm.get("candidates_ms", 0.0)},
             "candidates": cand,

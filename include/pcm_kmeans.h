@@ -183,6 +183,11 @@ int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *crowded_tiles, int64_
 int pcm_timing(pcm_engine *e, int enable);
 int pcm_timing_read(pcm_engine *e, double *ms /*[3]*/, int *count);
 
+/* Calibration: mean milliseconds of `reps` back-to-back assign launches on the
+ * current layout and centres, between one HIP event pair.  The statistics they
+ * add are discarded; the engine needs pcm_fit_begin before iterating again. */
+int pcm_time_assign(pcm_engine *e, int reps, void *stream, double *ms);
+
 /* Rows `rows[0..m)` (device int64) of the synthetic cloud, device float32[m*d]. */
 int pcm_synth_rows(float *out, const int64_t *rows, int64_t m, int d, uint64_t seed, void *stream);
 
