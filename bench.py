@@ -480,9 +480,9 @@ def main():
         # `steps` back-to-back assign launches on the final layout, lists and centres
         # (no per-launch events, no k_step between them; the statistics they add are
         # discarded -- nothing iterates this engine afterwards).  They run ~10 % faster
-        # than the same kernel inside the timed replay (rocprof, profiles/r4g_*): the
-        # final lists are built with smaller drift margins, and no k_step runs between,
-        # so the roofline keeps the eager-pass events, the closest to the timed region.
+        # than the same kernel inside the timed replay (rocprof, profiles/r4g_*) because
+        # the kernel gets cheaper as the fit settles (profiles/r4i_*), so the roofline
+        # keeps the eager-pass events, the closest to the timed region.
         b2b_ms = eng.time_assign(args.steps)
 
     fit = kpp_ms = None
