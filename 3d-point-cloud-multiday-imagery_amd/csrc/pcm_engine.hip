@@ -1508,7 +1508,9 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
         LAUNCHCHK();
         // from centre 64 on a step touches a neighbourhood: a quarter of the grid
         // (2048 -> 512 blocks) for eval/apply, 163.3 -> 159.1 ms at config 3
-        // (tools/kpp_grid_sweep.sh; 1/8: 162.6 ms).  PCM_KPP_LATE_*: tuning only
+        // (tools/kpp_grid_sweep.sh; 1/8: 162.6 ms); re-swept after the round-3
+        // atomics fix: 1/4 109.3-110.2, 1/2 113.3, 1/8 123.4 ms (tools/r4j.sh).
+        // PCM_KPP_LATE_*: tuning only
         static const int late_div = [] { const char *v = std::getenv("PCM_KPP_LATE_DIV"); return v ? std::max(1, std::atoi(v)) : 4; }();
         static const int late_c = [] { const char *v = std::getenv("PCM_KPP_LATE_C"); return v ? std::atoi(v) : 64; }();
         for (int c = 1; c < k; ++c) {
