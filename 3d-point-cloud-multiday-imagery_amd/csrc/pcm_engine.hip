@@ -407,11 +407,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->cref, (size_t)2 * k * sizeof(float4));
     err = err ? err : hipMalloc(&e->prev, nstat * sizeof(unsigned long long));
-#ifdef PCM_ABL_DOUBLE_FLUSH
-    err = err ? err : hipMalloc(&e->partials, (size_t)3 * k * (d + 1) * sizeof(unsigned long long));
-#else
     err = err ? err : hipMalloc(&e->partials, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
-#endif
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
     e->stats = e->stats_own;
     err = err ? err : hipMalloc(&e->held, nstat * sizeof(unsigned long long));
@@ -1030,23 +1026,34 @@ int pcm_time_assign(pcm_engine *e, int reps, void *stream, double *ms) {
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
     hipStream_t s = (hipStream_t)stream;
     if (int rc = timing_drain(e, true)) return rc;
-    const bool was = e->timing;
+    // a halted or finished fit gates k_lloyd1 off: its launches would time nothing
+    uint32_t flags[2] = {0u, 0u};
+    HIPCHK(hipMemcpyAsync(flags, e->ctrl, sizeof(flags), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (flags[0] | flags[1]) return fail(PCM_E_STATE, "the fit has halted or finished: nothing to time");
+    // events and the engine's timing flag are restored on every exit path
+    struct Guard {
+        pcm_engine *e;
+        bool was;
+        hipEvent_t a = nullptr, b = nullptr;
+        ~Guard() {
+            if (a) (void)hipEventDestroy(a);
+            if (b) (void)hipEventDestroy(b);
+            e->timing = was;
+        }
+    } g{e, e->timing};
     e->timing = false;
-    hipEvent_t a = nullptr, b = nullptr;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventCreate(&g.a));
+    HIPCHK(hipEventCreate(&g.b));
+    HIPCHK(hipEventRecord(g.a, s));
     int rc = 0;
-    HIPCHK(hipEventRecord(a, s));
     for (int i = 0; i < reps && !rc; ++i) rc = iter_local_impl(e, s, false);
-    HIPCHK(hipEventRecord(b, s));
-    HIPCHK(hipEventSynchronize(b));
-    float t = 0.f;
-    HIPCHK(hipEventElapsedTime(&t, a, b));
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
-    e->timing = was;
     e->fit_ready = false;   // the partial statistics now hold extra sums
     if (rc) return rc;
+    HIPCHK(hipEventRecord(g.b, s));
+    HIPCHK(hipEventSynchronize(g.b));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, g.a, g.b));
     *ms = (double)t / reps;
     return 0;
 }

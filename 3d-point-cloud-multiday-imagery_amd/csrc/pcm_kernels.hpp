@@ -785,9 +785,6 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     if (pfull) mp = (uint32_t)K;
     DBG_T(1);
     DBG_V(8, mp);
-#ifdef PCM_ABL_COARSEONLY
-    if (mp != 12345u) return;
-#endif
 
     // ---- 2. children (F = 4 per axis) of this block: c0 .. c1-1
     const int c0 = bsub * cpb, c1 = min(nchild, (bsub + 1) * cpb);
@@ -1468,11 +1465,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
     // gives 5 waves/SIMD) and at D = 4 (long lists are the norm there); the
     // 16-slot D <= 3 variant leaves them out (1.5 KB would cost a resident
     // block per CU) and sends the rare long list to global int64 atomics.
-#ifdef PCM_OVF_ALL
-    constexpr bool kOvf = true;
-#else
     constexpr bool kOvf = D >= 4 || LS <= 8;   // 8 slots: LDS int64 words past them; 12 / 16: global atomics (rare positions)
-#endif
     __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
     const int tid = threadIdx.x;
     const unsigned G = gridDim.x;
@@ -1562,11 +1555,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         float x[4][D];
         unpack_x<D>(cx, x);
         int bj[4];
-#ifdef PCM_ABL_NOSCAN
-        if (true) {
-#else
         if (h.mm == 1) {
-#endif
             for (int e = 0; e < 4; ++e) bj[e] = 0;
         } else {
             float bd[4];
@@ -1583,12 +1572,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
             over |= v && hi;
             sl[e] = (v && !hi) ? bj[e] : LS;
         }
-#ifdef PCM_ABL_NOACC
-        for (int e = 0; e < 4; ++e) sl[e] = (int)(x[e][0] * x[e][1] * x[e][2]) & 1;
-        for (int e = 0; e < 1; ++e) {
-#else
         for (int e = 0; e < 4; ++e) {
-#endif
             uint32_t *ap = myacc + sl[e] * ((D + 1) * AW);
             for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
             atomicAdd(ap + D * AW, 1u);
@@ -1623,11 +1607,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8)
         DBG_L(2);
         __syncthreads();
         {
-#ifdef PCM_ABL_NOFLUSH
-            const int nslots = 0;
-#else
             const int nslots = h.mm < LS ? h.mm : LS;
-#endif
             const int npairs = nslots * (D + 1);
             // 16 threads per (slot, a) row, each summing AW/16 of its words
             for (int p0 = 0; p0 < npairs; p0 += TPB / 16) {
@@ -1719,13 +1699,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     LloydArgs A, const uint4 *__restrict__ tiles, const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
     const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt, const float4 *__restrict__ tl_rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LS+1)*(D+1)][AW]
-    __shared__ float4 crec[CAPF];
-    __shared__ int32_t cid[CAPF];
-#ifdef PCM_OVF_ALL
-    constexpr bool kOvf = true;
-#else
-    constexpr bool kOvf = D >= 4 || LS <= 8;   // 8 slots: LDS int64 words past them; 12 / 16: global atomics (rare positions)
-#endif
+    // crowded layouts stage tile lists of up to TLCAP records in LDS (the long
+    // lists of clustered clouds scan from LDS instead of one scalar load per
+    // candidate) and sum list positions >= LS into the block-shared int64 words
+    // AccL::gwords (one global atomic per word and tile at the end, not one per point)
+    constexpr int LCAP = CROWD ? TLCAP : CAPF;
+    __shared__ float4 crec[LCAP];
+    __shared__ int32_t cid[LCAP];
+    // 8 slots (and D = 4): LDS int64 words past them; 12 / 16 slots: global atomics (rare positions)
+    constexpr bool kOvf = !CROWD && (D >= 4 || LS <= 8);
     __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
     const int tid = threadIdx.x;
     const unsigned t = blockIdx.x;
@@ -1752,13 +1734,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     }
     uint32_t cnt = fc_cnt[cell];
     // crowded cell (list FULL or past TL_MIN): the tile's own list when k_tile_cand built a shorter one
-    // (lists past CAPF: scanned from global memory like the all-K scan, Cs/glab)
     // (the all-K and long-list scans read through scalar loads of kernel
     // arguments: Call / tl_rec, never a selected pointer, which would turn them
     // into vector loads)
     const float4 *lrec = fc_rec + (size_t)cell * CAPF;
     const int32_t *llab = fc_lab + (size_t)cell * CAPF;
-    const int32_t *glab = nullptr;
     bool tl = false;
     if (CROWD && cnt > TL_MIN) {
         const uint32_t tc = A.tl_cnt[t];
@@ -1767,7 +1747,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             lrec = tl_rec + (size_t)t * TLCAP;
             llab = A.tl_lab + (size_t)t * TLCAP;
             tl = true;
-            if (tc > (uint32_t)CAPF) glab = llab;
         }
     }
     constexpr int NSUB = 1 << D;
@@ -1802,20 +1781,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         reinterpret_cast<unsigned long long *>(acc + (AccL<D, LS>::words + 1) / 2 * 2);
     if (kOvf)
         for (int e = tid; e < (CAPF - LS) * (D + 1); e += TPB) ovf[e] = 0ull;
-    const bool full = (cnt == FULL) || glab;
+    const bool full = (cnt == FULL);
     const int mm = (cnt == FULL) ? A.K : (int)cnt;
-    // long tile list: its centroid indices go to LDS, into crec's bytes (unused
-    // by the global scan: TLCAP int32 = CAPF float4), so the loop's label
-    // lookups stay LDS reads (a vector load there would make the waitcnt pass
-    // drain the point prefetch)
-    static_assert(TLCAP * sizeof(int32_t) <= CAPF * sizeof(float4), "long-list labels fit in crec");
-    int32_t *const glab_s = reinterpret_cast<int32_t *>(&crec[0]);
     if (full) {
-        if (tid < LS) cid[tid] = glab ? (tid < mm ? glab[tid] : 0) : tid;
-        if (glab) {
-            for (int j = tid; j < mm; j += TPB) glab_s[j] = glab[j];
-            for (int j = tid; j < mm * (D + 1); j += TPB) govf[j] = 0ull;
-        }
+        if (tid < LS) cid[tid] = tid;
+        // (crowded: positions >= LS of an all-K scan go to global atomics, as the 16-slot variant's)
     } else {
         if (tl) {   // block-uniform: crowded cells only (r0/l0 hold the cell list)
             if (tid < LSPEC && tid < mm) {
@@ -1830,6 +1800,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             crec[j] = lrec[j];
             cid[j] = llab[j];
         }
+        if (CROWD)
+            for (int j = LS * (D + 1) + tid; j < mm * (D + 1); j += TPB) govf[j] = 0ull;
     }
     uint32_t *const myacc = acc + (tid & (AW - 1));
     unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.pstride;
@@ -1910,9 +1882,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         __syncthreads();
     }
     DBG_L(1);
-#ifdef PCM_ABL_NOACC
-    int abl_sink = 0;
-#endif
 
     // loads per work item; after item r+2's are issued, items r+1 and r+2 may
     // stay outstanding while r is computed
@@ -1939,11 +1908,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             unpack_x<D>(cx, x);
         }
         int bj[4];
-#ifdef PCM_ABL_NOSCAN
-        if (true) {
-#else
         if (mm == 1) {
-#endif
             for (int e = 0; e < 4; ++e) bj[e] = 0;
         } else if (use_mask) {
             const unsigned long long m0 = rmask[r];
@@ -1959,8 +1924,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         } else {
             float bd[4];
             if (full) {
-                if (glab) scan4_s<D>(tl_rec + (size_t)t * TLCAP, mm, x, bd, bj);
-                else scan4_s<D>(Call, mm, x, bd, bj);
+                scan4_s<D>(Call, mm, x, bd, bj);
             } else {
                 scan4<D>(crec, mm, x, bd, bj);
             }
@@ -1975,24 +1939,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             over |= v && hi;
             sl[e] = (v && !hi) ? bj[e] : LS;
         }
-#ifdef PCM_ABL_NOACC
-        for (int e = 0; e < 4; ++e)
-            for (int a = 0; a < D; ++a) abl_sink += fixed_i(x[e][a], A.q[a]) + sl[e];
-        over = false;
-#else
         for (int e = 0; e < 4; ++e) {
             uint32_t *ap = myacc + sl[e] * ((D + 1) * AW);
             for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
             atomicAdd(ap + D * AW, 1u);
         }
-#endif
         if (over) {   // list positions >= LS (long lists only)
             for (int e = 0; e < 4; ++e) {
                 const bool v = whole || ((i0 + e >= start) && (i0 + e < end));
                 if (!(v && bj[e] >= LS)) continue;
                 // one address space per branch (a pointer select would make FLAT
                 // atomics, which count in vmcnt and lgkmcnt and drain the prefetch)
-                if (glab) {   // long tile list: block-shared words, folded at the end
+                if (CROWD && !full) {   // crowded list: block-shared words, folded at the end
                     unsigned long long *pp = govf + bj[e] * (D + 1);
                     for (int a = 0; a < D; ++a) atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
                     atomicAdd(pp + D, 1ull);
@@ -2018,9 +1976,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         step(xc, xb, r + 2);
     }
     DBG_L(2);
-#ifdef PCM_ABL_NOACC
-    if (abl_sink == 0x7fffffff) acc[0] = 1u;
-#endif
     // fold the slot words into the int64 statistics: 16 threads per (slot, a) row
     __syncthreads();
     {
@@ -2044,15 +1999,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             if (pi < npairs && sub == 0 && sacc) {
                 const int slot = pi / (D + 1), qq = pi % (D + 1);
                 atomicAdd(prep + (size_t)cid[slot] * (D + 1) + qq, (unsigned long long)sacc);
-#ifdef PCM_ABL_DOUBLE_FLUSH   // calibration build: the flush's atomics issued twice (a third, unused buffer)
-                atomicAdd(A.partials + 2 * A.pstride + (size_t)cid[slot] * (D + 1) + qq, (unsigned long long)sacc);
-#endif
             }
         }
-        if (glab)
+        if (CROWD && !full)
             for (int i = LS * (D + 1) + tid; i < mm * (D + 1); i += TPB) {
                 const unsigned long long w = govf[i];
-                if (w) atomicAdd(prep + (size_t)glab_s[i / (D + 1)] * (D + 1) + i % (D + 1), w);
+                if (w) atomicAdd(prep + (size_t)cid[i / (D + 1)] * (D + 1) + i % (D + 1), w);
             }
         if (kOvf && !full && mm > LS)
             for (int i = tid; i < (mm - LS) * (D + 1); i += TPB) {
@@ -2134,11 +2086,7 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
     if (lane == 0) { wmax[wv] = bmax; warg[wv] = barg; }
     if (ne) atomicAdd(&cnt_empty, ne);
     __syncthreads();
-#if defined(PCM_ABL_NOHALT)
-    if (false) {   // ablation build: never halt (statistics are meaningless)
-#else
     if (cnt_empty > 0 && !resume) {
-#endif
         // Snapshot the reduced statistics: the no-op iterations queued behind a
         // halt still run their all-reduce on `stats`.
         for (int i = tid; i < n + 1; i += 1024) held[i] = stats[i];
@@ -2233,9 +2181,6 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
             if (changed == 0ull) done = 1u;
             else if (shift <= ctrl->tol) done = 2u;
             ctrl->iter = it + 1;
-#if defined(PCM_ABL_NOHALT)
-            done = 0u;
-#endif
             if (!done && it + 1 >= ctrl->max_iter) done = 3u;
             ctrl->done = done;
         }
@@ -2377,11 +2322,7 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
         }
         if (halting && blockIdx.x == 0 && tid == 0) held[n] = 0ull;
     }
-#if defined(PCM_ABL_NOHALT)
-    const bool halt = false;   // ablation build: never halt (statistics are meaningless)
-#else
     const bool halt = s_empty > 0;
-#endif
     dmax = s_dmax[0];
     smax = s_smax[0];
     for (int w = 1; w < CAND_TPB / 64; ++w) { dmax = fmax(dmax, s_dmax[w]); smax = fmax(smax, s_smax[w]); }
@@ -2461,9 +2402,6 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
             uint32_t done = 0;
             if (changed == 0ull) done = 1u;
             else if (shift <= ctrl->tol) done = 2u;
-#if defined(PCM_ABL_NOHALT)
-            done = 0u;
-#endif
             if (!done && it + 1 >= ctrl->max_iter) done = 3u;
             ctrl->done = done;
             ctrl->iter = it + 1;

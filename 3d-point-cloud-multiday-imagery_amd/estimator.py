@@ -25,16 +25,21 @@ the boundary, which mirror sklearn's own NumPy calls.  Dtypes follow sklearn
 * D > 4, or float64 input the dense engine can take (the reference's
   1500 x 20 float64 call site): the dense engine (``dense.py``), computing in the
   input precision;
-* float64 point clouds (D <= 4) too large for brute force -- centres beyond
-  the dense engine's 64 KB LDS stage (K * D * 8 bytes; the dense engine itself
-  then reads them from L2) or more than 2**26 distance evaluations per
-  iteration (N * K) -- go to the pruned engine in float32 (the
-  boundary cast of the plugin path; its canonical fp32 fit equals sklearn's
-  float64 fit on pixel-unit height-map clouds, tests/test_plugin_cloud_golden.py).
+* float64 point clouds (D <= 4) stay float64 on the dense engine whatever
+  their size (as scikit-learn keeps float64).  ``float64_points="float32"`` opts
+  in to casting large ones -- centres beyond the dense engine's 64 KB LDS stage
+  (K * D * 8 bytes) or more than 2**26 distance evaluations per iteration
+  (N * K) -- to float32 for the pruned engine (the boundary cast of the plugin
+  path: its canonical fp32 fit equals sklearn's float64 fit on pixel-unit
+  height-map clouds, tests/test_plugin_cloud_golden.py; on general float64 data
+  labels may differ from sklearn's float64 fit, so the cast warns).  The
+  k-means++ first draw then still uses float64 unit weights, as sklearn's.
 """
 from __future__ import annotations
 
 from typing import Callable, Optional
+
+import warnings
 
 import numpy as np
 
@@ -51,8 +56,10 @@ class KMeans:
     """Drop-in for ``sklearn.cluster.KMeans`` (Lloyd, dense, unit weights) on MI355X."""
 
     def __init__(self, n_clusters: int = 8, *, init="k-means++", n_init="auto", max_iter: int = 300,
-                 tol: float = 1e-4, random_state=None, algorithm: str = "lloyd",
+                 tol: float = 1e-4, random_state=None, algorithm: str = "lloyd", float64_points: str = "dense",
                  _fit: Optional[Callable] = None, _seed: Optional[Callable] = None):
+        if float64_points not in ("dense", "float32"):
+            raise ValueError("float64_points must be 'dense' or 'float32'")
         self.n_clusters = n_clusters
         self.init = init
         self.n_init = n_init
@@ -60,6 +67,7 @@ class KMeans:
         self.tol = tol
         self.random_state = random_state
         self.algorithm = algorithm
+        self.float64_points = float64_points
         self._fit = _fit      # tests: a CPU stand-in for (Xc, C0, max_iter, tol) -> (labels, centers, inertia, n_iter)
         self._seed = _seed    # tests: a CPU stand-in for k-means++ (Xc, k, RandomState) -> centers
 
@@ -68,20 +76,21 @@ class KMeans:
     DENSE_MAX_EVALS = 1 << 26          # N * K distance evaluations per brute-force iteration
 
     @staticmethod
-    def _dense(X: np.ndarray, k: int) -> bool:
+    def _dense(X: np.ndarray, k: int, float64_points: str = "dense") -> bool:
         """Which engine fits X with k clusters: True = dense (input precision), False = pruned (float32)."""
         n, d = X.shape
         if d > 4:
             return True
         if X.dtype != np.float64:
             return False
+        if float64_points == "dense":
+            return True
         return k * d * 8 <= KMeans.DENSE_LDS_BYTES and n * k <= KMeans.DENSE_MAX_EVALS
 
-    @staticmethod
-    def _gpu_fit(Xc: np.ndarray, C0: np.ndarray, max_iter: int, tol: float):
+    def _gpu_fit(self, Xc: np.ndarray, C0: np.ndarray, max_iter: int, tol: float):
         import torch
 
-        if KMeans._dense(Xc, C0.shape[0]):
+        if KMeans._dense(Xc, C0.shape[0], self.float64_points):
             from .dense import dense_fit
             res = dense_fit(torch.from_numpy(Xc).cuda(), torch.from_numpy(np.ascontiguousarray(C0, Xc.dtype)).cuda(),
                             max_iter=max_iter, tol=tol)
@@ -93,16 +102,17 @@ class KMeans:
         torch.cuda.synchronize()
         return res.labels.cpu().numpy(), res.centers.cpu().numpy(), float(res.inertia), int(res.n_iter)
 
-    @staticmethod
-    def _gpu_seed(Xc: np.ndarray, k: int, rs: np.random.RandomState) -> np.ndarray:
+    def _gpu_seed(self, Xc: np.ndarray, k: int, rs: np.random.RandomState) -> np.ndarray:
         import torch
 
-        if KMeans._dense(Xc, k):
+        if KMeans._dense(Xc, k, self.float64_points):
             from .dense import dense_kmeanspp
             C, _ = dense_kmeanspp(torch.from_numpy(Xc).cuda(), k, random_state=rs)
         else:
             from .kpp import kmeans_plusplus
-            C, _ = kmeans_plusplus(torch.from_numpy(np.ascontiguousarray(Xc, np.float32)).cuda(), k, random_state=rs)
+            # sklearn's unit sample weights are in X's dtype: the first draw keeps them float64
+            C, _ = kmeans_plusplus(torch.from_numpy(np.ascontiguousarray(Xc, np.float32)).cuda(), k, random_state=rs,
+                                   weight_dtype=Xc.dtype)
         return C.cpu().numpy().astype(Xc.dtype)
 
     # ------------------------------------------------------------ sklearn API
@@ -122,6 +132,9 @@ class KMeans:
             raise ValueError("Input X contains NaN or infinity.")
         n, d = X.shape
         k = int(self.n_clusters)
+        if self._fit is None and dt == np.float64 and not KMeans._dense(X, k, self.float64_points):
+            warnings.warn("pcm_amd.KMeans: float64 points cast to float32 for the pruned engine (float64_points="
+                          "'float32'); labels may differ from a float64 fit", RuntimeWarning, stacklevel=2)
         if n < k:
             raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
         init = self.init

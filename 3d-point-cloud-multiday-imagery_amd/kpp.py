@@ -59,8 +59,11 @@ def _first_index(n: int, u0: float, weight_dtype=np.float32) -> int:
     return min(i, n - 1)
 
 
-def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_local_trials=None):
-    """GPU k-means++ of a (n, d) cloud on a HIP device; returns (centers (k, d) float32, indices int64)."""
+def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_local_trials=None,
+                    weight_dtype=None):
+    """GPU k-means++ of a (n, d) cloud on a HIP device; returns (centers (k, d) float32, indices int64).
+    ``weight_dtype``: dtype of sklearn's unit sample weights for the first draw (X's dtype by default;
+    the estimator passes float64 when it casts float64 points to float32)."""
     if not (isinstance(X, torch.Tensor) and X.is_cuda):
         raise _lib.PcmError("kmeans_plusplus expects a HIP device tensor (no CPU fallback)")
     if X.dim() != 2 or not 1 <= X.shape[1] <= 4:
@@ -79,7 +82,9 @@ def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_lo
         m = np.ldexp(u, 53)
         assert np.array_equal(np.ldexp(m, -53), u)      # random_sample doubles are multiples of 2**-53
         umant[(c - 1) * L:c * L] = m.astype(np.uint64)
-    first = _first_index(n, u0)
+    if weight_dtype is None:
+        weight_dtype = np.float64 if X.dtype == torch.float64 else np.float32
+    first = _first_index(n, u0, weight_dtype)
     idx = torch.empty(k, dtype=torch.int64, device=Xf.device)
     lib = _lib.load()
     nbytes = ctypes.c_size_t()

@@ -66,6 +66,29 @@ def _world(group):
 
 
 SLAB_BINS = 16384   # slab histogram resolution (pcm_shard_hist's LDS bound)
+SLAB_MAXP = 16      # PCM_SHARD_MAXP: ranks a slab partition can address (uint8 owner table, LDS counters)
+
+
+def slab_sizes(hist: np.ndarray, owner: np.ndarray, world: int) -> np.ndarray:
+    """Points each rank's slab receives (from the all-reduced histogram and the
+    owner table every rank holds: the same numbers on every rank)."""
+    return np.bincount(np.asarray(owner, np.int64), weights=np.asarray(hist, np.float64),
+                       minlength=world).astype(np.int64)
+
+
+def _build_all(engine, X, q, gidx0, world, group):
+    """engine.build on every rank; a failure on any rank raises on every rank
+    (MIN all-reduce of an ok flag), so no rank is left waiting in the next
+    collective."""
+    err = None
+    try:
+        engine.build(X, q, gidx0)
+    except Exception as exc:   # noqa: BLE001 -- re-raised below, after the ranks agree
+        err = exc
+    if not agree(err is None, world, group, engine.stats_device):
+        if err is not None:
+            raise err
+        raise RuntimeError("pcm_amd.lloyd: the layout build failed on another rank")
 
 
 def slab_owner(hist: np.ndarray, world: int) -> np.ndarray:
@@ -99,6 +122,10 @@ def prepare(engine, X, group=None, shard: str = "auto"):
         return q, n_local
     if shard not in ("auto", "slab", "rows"):
         raise ValueError("shard must be 'auto', 'slab' or 'rows'")
+    if world > SLAB_MAXP:
+        if shard == "slab":
+            raise ValueError(f"shard='slab' supports at most {SLAB_MAXP} ranks (world size {world}); use 'rows'")
+        shard = "rows"      # 'auto': row shards work at any world size
     dev = engine.stats_device
     mine = torch.tensor([n_local], dtype=torch.int64, device=dev)
     parts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
@@ -116,14 +143,22 @@ def prepare(engine, X, group=None, shard: str = "auto"):
     glo, ghi, maxabs = -m[:d], m[d:2 * d], m[2 * d:]
     q = fixed_q(maxabs)
     if shard == "rows" or n_total == 0:
-        engine.build(X, q, gidx0)
+        _build_all(engine, X, q, gidx0, world, group)
         return q, n_total
     ext = ghi - glo
     axis = int(np.argmax(ext))
     inv = SLAB_BINS / ext[axis] if ext[axis] > 0 else 0.0
     hist = engine.shard_hist(X, axis, glo[axis], inv, SLAB_BINS)
     dist.all_reduce(hist, group=group)
-    owner = slab_owner(hist.cpu().numpy(), world)
+    hist_h = hist.cpu().numpy()
+    owner = slab_owner(hist_h, world)
+    from .engine import ENGINE_MAX_POINTS
+    if int(slab_sizes(hist_h, owner, world).max()) > ENGINE_MAX_POINTS:
+        # a dense bin would overfill one rank's engine: every rank sees the same
+        # histogram and owner table, so all of them keep their row shards together
+        warnings.warn("pcm_amd.lloyd: a spatial slab would exceed one engine's capacity; keeping row shards")
+        _build_all(engine, X, q, gidx0, world, group)
+        return q, n_total
     Xs, rows, send = engine.shard_partition(X, axis, glo[axis], inv, SLAB_BINS, owner, world, gidx0)
     st = torch.tensor(send, dtype=torch.int64, device=dev)
     rt = torch.empty_like(st)
@@ -137,7 +172,7 @@ def prepare(engine, X, group=None, shard: str = "auto"):
     del Xs
     engine.bbox(Xr)
     engine.set_shard(rows_r, n_total)
-    engine.build(Xr, q, 0)
+    _build_all(engine, Xr, q, 0, world, group)
     engine._slab = dict(rows=rows, send=sl, recv=rl, gidx0=gidx0, n_local=n_local, axis=axis,
                         n_slab=sum(rl))
     return q, n_total

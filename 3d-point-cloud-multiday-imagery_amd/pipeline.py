@@ -52,8 +52,8 @@ class CropFailed(RuntimeError):
 
 GATHER_NAMES = ("left_right_consistency", "photoconsistency_map")
 _gather_lock = threading.Lock()
-_gather_users = 0
-_gather_saved: dict = {}
+_gather_users: dict = {}     # id(module) -> active use_gpu_gathers blocks on that module
+_gather_saved: dict = {}     # id(module) -> {name: original binding} (names the module had)
 
 
 @contextlib.contextmanager
@@ -61,27 +61,27 @@ def use_gpu_gathers(module):
     """Rebind ``module.left_right_consistency`` / ``module.photoconsistency_map``
     (the globals ``disparity_map`` resolves at ``disparity.py:157-161``) to the HIP
     drop-ins for the duration of the block; restored on exit (also on error).
-    Reference-counted, so concurrent plugin runs share one binding."""
-    global _gather_users
+    Reference-counted per module, so concurrent plugin runs share one binding and
+    each module gets back exactly its own originals."""
     from . import stereo
+    key = id(module)
     with _gather_lock:
-        if _gather_users == 0:
-            _gather_saved.clear()
+        if _gather_users.get(key, 0) == 0:
+            _gather_saved[key] = {name: getattr(module, name) for name in GATHER_NAMES if hasattr(module, name)}
             for name in GATHER_NAMES:
-                if hasattr(module, name):
-                    _gather_saved[(id(module), name)] = getattr(module, name)
                 setattr(module, name, getattr(stereo, name))
-        _gather_users += 1
+        _gather_users[key] = _gather_users.get(key, 0) + 1
     try:
         yield module
     finally:
         with _gather_lock:
-            _gather_users -= 1
-            if _gather_users == 0:
+            _gather_users[key] -= 1
+            if _gather_users[key] == 0:
+                del _gather_users[key]
+                saved = _gather_saved.pop(key, {})
                 for name in GATHER_NAMES:
-                    key = (id(module), name)
-                    if key in _gather_saved:
-                        setattr(module, name, _gather_saved.pop(key))
+                    if name in saved:
+                        setattr(module, name, saved[name])
                     else:
                         delattr(module, name)
 
@@ -200,15 +200,19 @@ class ReferenceStereoStages:
                                                                 C.TMP_CROPPED_IMAGES_PATH, C.TMP_DISPARITY_DEBUG_PATH)
             self.log("Disparity map generated successfully")
             image_layers = []
-            if is_debug_mode:   # plugin.py:119-145
-                sources = [(os.path.join(C.TMP_CROPPED_IMAGES_PATH, pair.img1.cropped_name), "Input Left"),
-                           (os.path.join(C.TMP_CROPPED_IMAGES_PATH, pair.img2.cropped_name), "Input Right"),
+            if is_debug_mode:   # plugin.py:120-145
+                self.log("Loading  basic cropped image for display...")
+                # the cropped inputs are opened unconditionally (plugin.py:123, 128): a missing
+                # crop raises and becomes the reference's "Error: ..." layer; the rectified
+                # images only when present (plugin.py:134, 141)
+                sources = [(os.path.join(C.TMP_CROPPED_IMAGES_PATH, pair.img1.cropped_name), "Input Left", True),
+                           (os.path.join(C.TMP_CROPPED_IMAGES_PATH, pair.img2.cropped_name), "Input Right", True),
                            (os.path.join(C.TMP_STEREO_OUTPUT_PATH, str(pair_id), "results", "out-L.tif"),
-                            "Rectified Left"),
+                            "Rectified Left", False),
                            (os.path.join(C.TMP_STEREO_OUTPUT_PATH, str(pair_id), "results", "out-R.tif"),
-                            "Rectified Right")]
-                for path, label in sources:
-                    if os.path.exists(path):
+                            "Rectified Right", False)]
+                for path, label, required in sources:
+                    if required or os.path.exists(path):
                         im = open_tiff_file(path)
                         image_layers.append((normalise_for_display(im, im > 0),
                                              {"name": f"{PREFIX} {label}", "colormap": "gray"}, "image"))

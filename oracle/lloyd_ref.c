@@ -97,6 +97,18 @@ int64_t ref_lloyd_stats(const float *X, int64_t n, int d, const float *C, int k,
                         bestd[p] = m ? acc : bestd[p];
                         bestj[p] = m ? j : bestj[p];
                     }
+                } else if (d == 4) {   /* config 5: the same canonical order, vectorised over the block */
+#pragma omp simd
+                    for (int p = 0; p < PB; ++p) {
+                        float e0 = xs[0][p] - c0, e1 = xs[1][p] - c1, e2 = xs[2][p] - c2, e3 = xs[3][p] - c3;
+                        float s0 = e0 * e0, s1 = e1 * e1, s2 = e2 * e2, s3 = e3 * e3;
+                        float acc = s0 + s1;
+                        acc = acc + s2;
+                        acc = acc + s3;
+                        int m = acc < bestd[p];
+                        bestd[p] = m ? acc : bestd[p];
+                        bestj[p] = m ? j : bestj[p];
+                    }
                 } else {
                     for (int p = 0; p < PB; ++p) {
                         float e0 = xs[0][p] - c0;

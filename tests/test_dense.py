@@ -199,9 +199,33 @@ def test_estimator_engine_routing():
     assert KMeans._dense(f64, 5)                                    # the call site: dense, float64
     assert KMeans._dense(np.zeros((1000, 3)), 8)                    # small float64 cloud: dense
     assert not KMeans._dense(f32, 8)                                # float32 cloud: pruned engine
-    assert not KMeans._dense(np.zeros((1000, 3)), 4096)             # K*D*8 > 64 KB: pruned (float32)
-    assert not KMeans._dense(np.zeros((200_000, 4)), 1024)          # N*K > 2^26: pruned
+    assert KMeans._dense(np.zeros((1000, 3)), 4096)                 # float64 stays float64 (dense) by default
+    assert KMeans._dense(np.zeros((200_000, 4)), 1024)
+    assert not KMeans._dense(np.zeros((1000, 3)), 4096, "float32")  # opt-in cast: K*D*8 > 64 KB -> pruned
+    assert not KMeans._dense(np.zeros((200_000, 4)), 1024, "float32")   # N*K > 2^26 -> pruned
+    assert KMeans._dense(np.zeros((1000, 3)), 8, "float32")         # small float64 cloud: dense either way
     assert KMeans._dense(np.zeros((10, 5), np.float32), 3)          # D > 4: dense whatever the dtype
+    with pytest.raises(ValueError):
+        KMeans(4, float64_points="half")
+
+
+def test_estimator_float32_cast_warns_and_keeps_float64_first_draw(monkeypatch):
+    """The opt-in float32 cast warns, and the k-means++ first draw uses float64 unit weights."""
+    from pcm_amd import estimator
+    seen = {}
+
+    def fake_seed(self, Xc, k, rs):
+        seen["dtype"] = Xc.dtype
+        return Xc[:k].copy()
+
+    def fake_fit(self, Xc, C0, max_iter, tol):
+        return np.zeros(len(Xc), np.int32), C0, 0.0, 1
+    monkeypatch.setattr(estimator.KMeans, "_gpu_seed", fake_seed)
+    monkeypatch.setattr(estimator.KMeans, "_gpu_fit", fake_fit)
+    X = np.random.default_rng(0).random((70_000, 3))
+    with pytest.warns(RuntimeWarning, match="float32"):
+        estimator.KMeans(1024, float64_points="float32", n_init=1).fit(X)
+    assert seen["dtype"] == np.float64
 
 
 def test_estimator_rejects_nonfinite_before_any_device_call():
@@ -217,19 +241,37 @@ def test_estimator_rejects_nonfinite_before_any_device_call():
 
 @pytest.mark.gpu
 def test_gpu_estimator_float64_cloud_large_k(gpu):
-    """float64 D=3 cloud with K=4096 (beyond the dense engine's LDS stage): the
-    estimator routes it to the pruned engine (float32) and fits; labels equal the
-    oracle's canonical fit of the float32-cast centred cloud."""
+    """float64 D=3 cloud with K=4096 (beyond the dense engine's LDS stage) and the
+    opt-in float32 cast: the estimator routes it to the pruned engine and fits;
+    labels equal the oracle's canonical fit of the float32-cast centred cloud."""
     from pcm_amd.estimator import KMeans
     from oracle import lloyd_ref as R
     rng = np.random.default_rng(5)
     X = rng.random((60_000, 3)) * np.array([30.0, 1500.0, 2200.0])
     init = X[np.sort(rng.choice(len(X), 4096, replace=False))]
-    km = KMeans(4096, init=init, n_init=1, max_iter=15, tol=0.0).fit(X)
+    with pytest.warns(RuntimeWarning):
+        km = KMeans(4096, init=init, n_init=1, max_iter=15, tol=0.0, float64_points="float32").fit(X)
     Xc = X - X.mean(axis=0)
     ref = R.lloyd_fit(Xc.astype(np.float32), (init - X.mean(axis=0)).astype(np.float32), max_iter=15, tol=0.0,
                       fast=True)
     np.testing.assert_array_equal(km.labels_, ref["labels"])
+    assert km.n_iter_ == ref["n_iter"] and km.cluster_centers_.dtype == np.float64
+
+
+@pytest.mark.gpu
+def test_gpu_estimator_float64_cloud_large_k_stays_float64(gpu):
+    """Default routing: a float64 D=3 cloud with K*D*8 > 64 KB and
+    N*K > 2^26 stays float64 on the dense engine; the fit equals the float64
+    dense oracle on the centred cloud (labels, centres, n_iter)."""
+    from pcm_amd.estimator import KMeans
+    rng = np.random.default_rng(6)
+    X = rng.random((40_000, 3)) * np.array([30.0, 1500.0, 2200.0])
+    init = X[np.sort(rng.choice(len(X), 3000, replace=False))]
+    km = KMeans(3000, init=init, n_init=1, max_iter=6, tol=0.0).fit(X)
+    mu = X.mean(axis=0)
+    ref = DR.dense_fit(X - mu, init - mu, max_iter=6, tol=0.0)
+    np.testing.assert_array_equal(km.labels_, ref["labels"])
+    np.testing.assert_array_equal(km.cluster_centers_, ref["centers"] + mu)
     assert km.n_iter_ == ref["n_iter"] and km.cluster_centers_.dtype == np.float64
 
 

@@ -28,19 +28,34 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False, shard="auto"):
+def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False, shard="auto", opts=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import pcm_amd
     from cpu_engine import OracleEngine
-    from pcm_amd.lloyd import LOCAL
+    from pcm_amd import engine as E
+    from pcm_amd import lloyd as L
+    opts = opts or {}
+    if "maxp" in opts:
+        L.SLAB_MAXP = opts["maxp"]
+    if "engine_cap" in opts:
+        E.ENGINE_MAX_POINTS = opts["engine_cap"]
     n = X.shape[0]
     a, b = (0, n) if local else (n * rank // world, n * (rank + 1) // world)
     eng = OracleEngine(X.shape[1], C0.shape[0], max_iter)
-    res = pcm_amd.lloyd_fit(torch.from_numpy(X[a:b]), torch.from_numpy(C0), max_iter=max_iter, tol=0.0,
-                            chunk=chunk, engine=eng, group=LOCAL if local else None, shard=shard)
+    if opts.get("fail_build_rank") == rank:
+        def bad_build(*args, **kw):
+            raise RuntimeError("injected build failure")
+        eng.build = bad_build
+    try:
+        res = pcm_amd.lloyd_fit(torch.from_numpy(X[a:b]), torch.from_numpy(C0), max_iter=max_iter, tol=0.0,
+                                chunk=chunk, engine=eng, group=L.LOCAL if local else None, shard=shard)
+    except Exception as exc:   # noqa: BLE001 -- the test inspects every rank's outcome
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), error=f"{type(exc).__name__}: {exc}")
+        dist.destroy_process_group()
+        return
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), labels=res.labels.numpy(), centers=res.centers.numpy(),
              n_iter=res.n_iter, inertia=res.inertia, changed=res.changed, relocs=res.relocations,
              shard=res.layout.get("shard", "rows"), slab_points=res.layout.get("slab_points", -1))
@@ -48,9 +63,9 @@ def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False, sha
     dist.destroy_process_group()
 
 
-def run_world(X, C0, max_iter, chunk, tmp_path, world=2, local=False, shard="auto"):
+def run_world(X, C0, max_iter, chunk, tmp_path, world=2, local=False, shard="auto", opts=None):
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, X, C0, max_iter, chunk, str(tmp_path), local, shard), nprocs=world,
+    mp.spawn(_worker, args=(world, port, X, C0, max_iter, chunk, str(tmp_path), local, shard, opts), nprocs=world,
              join=True)
     parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
     return parts
@@ -139,3 +154,52 @@ def test_three_ranks_skewed_slabs(tmp_path):
         np.testing.assert_array_equal(p["centers"], ref["centers"])
         assert int(p["n_iter"]) == ref["n_iter"]
         assert float(p["inertia"]) == ref["inertia"]
+
+
+# ---------------------------------------------------------------- ADVICE r3 (slab limits, build failures)
+def _check_fit(parts, ref):
+    labels = np.concatenate([p["labels"] for p in parts])
+    np.testing.assert_array_equal(labels, ref["labels"])
+    for p in parts:
+        np.testing.assert_array_equal(p["centers"], ref["centers"])
+        assert int(p["n_iter"]) == ref["n_iter"]
+
+
+def test_auto_falls_back_to_rows_past_the_slab_rank_limit(tmp_path):
+    """More ranks than a slab partition addresses (PCM_SHARD_MAXP, lowered here
+    to 1): shard='auto' keeps row shards, shard='slab' raises on every rank."""
+    from oracle import lloyd_ref as R
+    X = R.splitmix_uniform(4000, 3, 25)
+    C0 = X[R.init_indices(4000, 10)]
+    ref = R.lloyd_fit(X, C0, max_iter=8)
+    parts = run_world(X, C0, 8, 4, tmp_path, opts={"maxp": 1})
+    assert all(str(p["shard"]) == "rows" for p in parts)
+    _check_fit(parts, ref)
+    parts = run_world(X, C0, 8, 4, tmp_path, shard="slab", opts={"maxp": 1})
+    assert all("ValueError" in str(p["error"]) for p in parts)
+
+
+def test_oversized_slab_keeps_row_shards_on_every_rank(tmp_path):
+    """A slab larger than one engine holds (the cap lowered to 2500 points; each
+    of the two slabs would get 3000): every rank sees the same histogram and
+    keeps its row shard, and the fit is unchanged."""
+    from oracle import lloyd_ref as R
+    X = R.splitmix_uniform(6000, 3, 26)
+    C0 = X[R.init_indices(6000, 16)]
+    ref = R.lloyd_fit(X, C0, max_iter=10)
+    parts = run_world(X, C0, 10, 4, tmp_path, opts={"engine_cap": 2500})
+    assert all(str(p["shard"]) == "rows" for p in parts)
+    _check_fit(parts, ref)
+
+
+def test_build_failure_on_one_rank_raises_on_every_rank(tmp_path):
+    """engine.build failing on rank 1 only: both ranks raise (rank 0 learns it
+    from the agreement all-reduce) instead of rank 0 blocking in the next
+    collective."""
+    from oracle import lloyd_ref as R
+    X = R.splitmix_uniform(3000, 3, 27)
+    C0 = X[R.init_indices(3000, 8)]
+    for shard in ("slab", "rows"):
+        parts = run_world(X, C0, 5, 4, tmp_path, shard=shard, opts={"fail_build_rank": 1})
+        assert "injected build failure" in str(parts[1]["error"])
+        assert "another rank" in str(parts[0]["error"])

@@ -85,7 +85,12 @@ def fake_reference(tmp_path, monkeypatch):
     pkg["members.rafael.disparity.preprocessing"].get_crop_area_from_kml = get_crop_area_from_kml
     pkg["members.rafael.disparity.preprocessing"].generate_cropped = generate_cropped
     pkg["members.rafael.disparity.processing"].generate_rectified = lambda pair, pid, out: out
-    pkg["members.rafael.disparity.utils"].open_tiff_file = lambda p: np.ones((4, 4))
+    def open_tiff_file(path):
+        if seen.get("missing_crop") and os.path.basename(path) == seen["missing_crop"]:
+            raise FileNotFoundError(f"No such file: {path}")
+        return np.ones((4, 4))
+
+    pkg["members.rafael.disparity.utils"].open_tiff_file = open_tiff_file
 
     D = pkg["members.rafael.disparity.disparity"]
     D.left_right_consistency = _ref_lrc
@@ -173,3 +178,35 @@ def test_use_gpu_gathers_refcount():
             assert m.left_right_consistency is stereo.left_right_consistency
         assert m.photoconsistency_map is stereo.photoconsistency_map     # still held by the outer user
     assert m.left_right_consistency is _ref_lrc and m.photoconsistency_map is _ref_photo
+
+
+def test_debug_images_logged_and_missing_crop_is_an_error_layer(fake_reference):
+    """plugin.py:120-131: the debug branch logs "Loading  basic cropped image for
+    display..." and opens the cropped Input Left/Right unconditionally, so a
+    missing crop raises and becomes the reference's "Error: ..." layer."""
+    out = _plugin().run("roi.kml", is_debug_mode=True)
+    names = [l[1]["name"] for l in out]
+    assert any(n.endswith("Input Left") for n in names) and any(n.endswith("Input Right") for n in names)
+    log = open(os.path.join(fake_reference["temp"], "log.txt")).read()
+    assert "Loading  basic cropped image for display..." in log
+    fake_reference["seen"]["missing_crop"] = "b.tif"
+    out = _plugin().run("roi.kml", is_debug_mode=True)
+    assert len(out) == 1 and out[0][1]["name"].startswith("Error: No such file") and (out[0][0] == 1).all()
+
+
+def test_use_gpu_gathers_refcount_per_module():
+    """Two modules rebound in interleaved blocks: each gets back its own originals
+    (one shared count restored the wrong module)."""
+    from pcm_amd import stereo
+    a, b = types.ModuleType("fake_a"), types.ModuleType("fake_b")
+    a.left_right_consistency, a.photoconsistency_map = _ref_lrc, _ref_photo
+    b.photoconsistency_map = _ref_photo          # b lacks left_right_consistency
+    ca, cb = pipeline.use_gpu_gathers(a), pipeline.use_gpu_gathers(b)
+    ca.__enter__()
+    cb.__enter__()
+    assert b.left_right_consistency is stereo.left_right_consistency
+    ca.__exit__(None, None, None)                # a restored while b is still rebound
+    assert a.left_right_consistency is _ref_lrc and a.photoconsistency_map is _ref_photo
+    assert b.photoconsistency_map is stereo.photoconsistency_map
+    cb.__exit__(None, None, None)
+    assert b.photoconsistency_map is _ref_photo and not hasattr(b, "left_right_consistency")

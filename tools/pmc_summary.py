@@ -52,6 +52,13 @@ def main():
         out["hbm_read_bytes_corrected"] = out["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in out:
         out["hbm_write_bytes"] = out["WRITE_SIZE"] * 1024
+    if "GRBM_GUI_ACTIVE" in out and out.get("_ns"):
+        out["clock_GHz"] = out["GRBM_GUI_ACTIVE"] / 8 / out["_ns"]   # summed over the 8 XCDs
+    if "SQ_WAVE_CYCLES" in out:   # fractions of the waves' (quad-)cycles
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                  "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS"):
+            if k in out:
+                out["frac_" + k] = out[k] / out["SQ_WAVE_CYCLES"]
     print(json.dumps(out, indent=1, sort_keys=True))
 
 
