@@ -89,8 +89,12 @@ struct pcm_engine {
     float4 *fc_rec = nullptr;
     int32_t *fc_lab = nullptr;
     float4 *C = nullptr, *Cn = nullptr;
-    float4 *cref = nullptr;                    // [2][K] reference centres of the candidate lists (k_step)
-    double drift_alpha = 2.0, drift_kappa = 0.05;  // candidate-list reuse policy (see k_step)
+    float4 *cref = nullptr;                    // [2][K] reference centres of the candidate lists (k_upd / k_lists)
+    double *shbuf = nullptr;                   // [K] squared centre shifts of one iteration (k_upd's shift tree)
+    uint32_t *cl_cnt = nullptr;                // [ncoarse] coarse candidate lists (k_coarse; split layouts)
+    int32_t *cl_idx = nullptr;                 // [ncoarse][cand_capc]
+    size_t cap_clc = 0, cap_cli = 0;
+    double drift_alpha = 2.0, drift_kappa = 0.05;  // candidate-list reuse policy (see k_upd)
     unsigned long long *prev = nullptr;        // raw statistics of the previous iteration
     int iscale = 0;                  // exact-inertia weight exponent (from the global q)
     unsigned long long *partials = nullptr, *stats = nullptr, *hist_changed = nullptr;
@@ -243,7 +247,8 @@ void free_layout(pcm_engine *e) {
 
 void free_buffers(pcm_engine *e) {
     void *ps[] = {e->xs, e->perm, e->lab, e->cell_start, e->tiles, e->fc_cnt, e->fc_rec, e->fc_lab, e->tile_off, e->ws,
-                  e->sub_start, e->xz, e->tmeta, e->tbox, e->tl_cnt, e->tl_rec, e->tl_lab, e->zcnt, e->dmap};
+                  e->sub_start, e->xz, e->tmeta, e->tbox, e->tl_cnt, e->tl_rec, e->tl_lab, e->zcnt, e->dmap,
+                  e->cl_cnt, e->cl_idx};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     e->dmap = nullptr; e->cap_dmap = 0; e->has_dmap = false;
@@ -253,6 +258,7 @@ void free_buffers(pcm_engine *e) {
     e->tbox = nullptr; e->tl_cnt = nullptr; e->tl_rec = nullptr; e->tl_lab = nullptr; e->zcnt = nullptr;
     e->cap_tbox = e->cap_tlc = e->cap_tlr = e->cap_tll = e->cap_zcnt = 0; e->zlev = 0;
     e->fc_cnt = nullptr; e->fc_rec = nullptr; e->fc_lab = nullptr;
+    e->cl_cnt = nullptr; e->cl_idx = nullptr; e->cap_clc = e->cap_cli = 0;
     e->cap_xs = e->cap_lab = e->cap_perm = e->cap_cells = e->cap_fc = e->cap_tiles = e->cap_ws = 0;
     free_layout(e);
 }
@@ -406,6 +412,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->C, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->cref, (size_t)2 * k * sizeof(float4));
+    err = err ? err : hipMalloc(&e->shbuf, (size_t)k * sizeof(double));
     err = err ? err : hipMalloc(&e->prev, nstat * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->partials, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
@@ -441,7 +448,7 @@ int pcm_engine_destroy(pcm_engine *e) {
         for (int j = 0; j < 4; ++j)
             if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
     free_buffers(e);
-    void *ps[] = {e->C, e->Cn, e->cref, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
+    void *ps[] = {e->C, e->Cn, e->cref, e->shbuf, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
                   e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx, e->ntiles_dev,
                   e->grows, e->zpts};
     for (void *p : ps)
@@ -744,7 +751,7 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
     e->ctrl_host.tol = tol;
     HIPCHK(hipMemcpyAsync(e->ctrl, &e->ctrl_host, sizeof(Ctrl), hipMemcpyHostToDevice, s));
     e->fit_ready = true;
-    // candidate lists of C0 (later iterations get theirs from k_step / the resume path)
+    // candidate lists of C0 (later iterations get theirs from k_lists / the resume path)
     return launch_candidates(e, s, 0);
 }
 
@@ -764,12 +771,34 @@ static int cand_bpc(const pcm_engine *e) {
     return (int)std::max(1LL, std::min(8LL, b));
 }
 
+// Coarse cells split over many blocks (D = 4: 256 children, 32 blocks each)
+// get their coarse list computed once, by k_coarse, instead of once per block
+// (config-5 shard: the same K = 4096 pruning pass 32 times per coarse cell).
+static bool split_coarse(const pcm_engine *e) { return e->g.prune && cand_bpc(e) >= 8; }
+
+// coarse-list storage of the current layout (split layouts only)
+static int ensure_coarse(pcm_engine *e) {
+    if (!split_coarse(e)) return 0;
+    const int cap = e->d >= 4 ? cand_capc<4>() : cand_capc<3>();
+    HIPCHK(ensure(e->cl_cnt, e->cap_clc, (size_t)e->g.ncoarse * sizeof(uint32_t)));
+    HIPCHK(ensure(e->cl_idx, e->cap_cli, (size_t)e->g.ncoarse * cap * sizeof(int32_t)));
+    return 0;
+}
+
 static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
         const int bpc = cand_bpc(e);
+        CoarseL cl;
+        if (split_coarse(e)) {
+            if (int rc = ensure_coarse(e)) return rc;
+            k_coarse<D><<<(int)e->g.ncoarse, CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->ctrl, 0, e->cl_cnt, e->cl_idx);
+            LAUNCHCHK();
+            cl.in_cnt = e->cl_cnt;
+            cl.in_idx = e->cl_idx;
+        }
         k_cand<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
-                                                                 e->ctrl, gate, bpc, e->cref);
+                                                                 e->ctrl, gate, bpc, e->cref, cl);
         LAUNCHCHK();
         return 0;
     });
@@ -811,6 +840,13 @@ static int lloyd_slots(const pcm_engine *e) {
     // cells per centre of the whole cloud (a spatial shard's cells cover ~n / n_global of the centres)
     const double share = e->n_global > 0 ? std::min(1.0, (double)e->n / (double)e->n_global) : 1.0;
     return (e->g.prune && (double)e->g.ncells >= 8.0 * e->k * share) ? 8 : LSLOT;
+}
+
+// Lane slots of the launched k_lloyd1: 8 on fine grids at D <= 3 (and at D = 4
+// with PCM_D4_LS8=1, a tuning switch), else LSLOT.
+static int assign_ls(const pcm_engine *e) {
+    static const bool d4_ls8 = [] { const char *v = std::getenv("PCM_D4_LS8"); return v && std::atoi(v); }();
+    return ((e->d <= 3 || d4_ls8) && lloyd_slots(e) == 8) ? 8 : LSLOT;
 }
 
 static LloydArgs lloyd_args(pcm_engine *e) {
@@ -900,9 +936,9 @@ static int timing_mark(pcm_engine *e, int which, hipStream_t s) {
     return 0;
 }
 
-// k_lloyd (its candidate lists were built by the previous k_step, the resume
+// k_lloyd (its candidate lists were built by the previous k_lists, the resume
 // path or pcm_fit_begin).  to_stats: accumulate straight into `stats` (the
-// all-reduce buffer, zeroed by the previous k_step / k_global / fit_begin);
+// all-reduce buffer, zeroed by the previous k_upd / k_global / fit_begin);
 // otherwise into the single-GPU parity half partials[iter & 1].
 static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
     if (int rc = timing_mark(e, 0, s)) return rc;
@@ -937,7 +973,7 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
             };
             // coarse grids keep 16 slots with masks: 8 slots + LDS int64 words 42.0 -> 51.2 us,
             // 12 slots + global atomics 42.6 -> 65.7 us at 12.5M (tools/mls_sweep.sh)
-            if (D <= 3 && lloyd_slots(e) == 8) launch(std::integral_constant<int, 8>{});
+            if (assign_ls(e) == 8) launch(std::integral_constant<int, 8>{});
             else launch(std::integral_constant<int, LSLOT>{});
             LAUNCHCHK();
         }
@@ -952,41 +988,37 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
 }
 
 // Centre update + next candidate lists.  stats_in: the all-reduced statistics
-// (multi-GPU / resume) or nullptr (single GPU: partials[parity]).  K <=
-// KSTEP_MAX: one fused k_step launch; otherwise k_global then k_cand.  The
-// relocation resume always takes k_global (it handles `resume`) + k_cand.
-static int kstep_max() {
-    static const int v = [] {
-        const char *ov = std::getenv("PCM_KSTEP_MAX");   // tuning sweeps only
-        return ov ? std::min(KSTEP_MAX, std::atoi(ov)) : KSTEP_MAX;
-    }();
-    return v;
-}
-
+// (multi-GPU) or nullptr (single GPU: partials[parity]).  Every K: k_upd (the
+// K new centres once, convergence, history) then k_lists (C := new centres,
+// this block's lists rebuilt or refreshed).  The relocation resume takes
+// k_global (it handles `resume`) + k_cand.
 static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bool resume_path) {
     int rc = dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        if (e->k <= kstep_max() && !resume_path) {
-            const int bpc = cand_bpc(e);
-            const size_t lds = (size_t)e->k * sizeof(float4);
-            static bool attr_set[MAXD + 1] = {false, false, false, false, false};
-            if (lds > 32768 && !attr_set[D]) {
-                HIPCHK(hipFuncSetAttribute((const void *)k_step<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(KSTEP_MAX * sizeof(float4))));
-                attr_set[D] = true;
-            }
+        if (!resume_path) {
             double wmin = 0.0;
             for (int a = 0; a < D; ++a)
                 if (e->g.ext[a] > 0 && (wmin == 0.0 || e->g.w[a] < wmin)) wmin = e->g.w[a];
-            k_step<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, lds, s>>>(
-                e->g, from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->cref,
-                e->hist_changed, e->hist_shift, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab, bpc, e->drift_alpha,
-                e->drift_kappa * wmin);
+            k_upd<D><<<blocks_for(e->k, UPD_TPB), UPD_TPB, 0, s>>>(
+                from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->Cn, e->cref,
+                e->shbuf, e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin);
+            LAUNCHCHK();
+            const int bpc = cand_bpc(e);
+            CoarseL cl;
+            if (split_coarse(e)) {
+                if (int rc = ensure_coarse(e)) return rc;
+                k_coarse<D><<<(int)e->g.ncoarse, CAND_TPB, 0, s>>>(e->g, e->Cn, e->k, e->ctrl, 1, e->cl_cnt, e->cl_idx);
+                LAUNCHCHK();
+                cl.in_cnt = e->cl_cnt;
+                cl.in_idx = e->cl_idx;
+            }
+            k_lists<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl,
+                                                                       e->fc_cnt, e->fc_rec, e->fc_lab, bpc, cl);
             LAUNCHCHK();
             return 0;
         }
-        k_global<D><<<1, 1024, 0, s>>>(from_partials ? e->partials : nullptr, e->stats, e->k, e->qe, e->held, e->prev,
-                                       e->C, e->Cn, e->hist_changed, e->hist_shift, e->ctrl);
+        k_global<D><<<1, 1024, 0, s>>>(nullptr, e->stats, e->k, e->qe, e->held, e->prev, e->C, e->Cn,
+                                       e->hist_changed, e->hist_shift, e->ctrl);
         LAUNCHCHK();
         return launch_candidates(e, s, 1);
     });
@@ -1058,7 +1090,7 @@ int pcm_time_assign(pcm_engine *e, int reps, void *stream, double *ms) {
     return 0;
 }
 
-// Single-process iterations: the fold is fused into k_global (3 launches per iteration).
+// Single-process iterations: k_lloyd1 into partials[parity], k_upd, k_lists.
 int pcm_iterate(pcm_engine *e, int n, void *stream) {
     if (!e || n < 0) return fail(PCM_E_ARG, "bad argument");
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
@@ -1285,7 +1317,7 @@ int pcm_layout_stream_bytes(pcm_engine *e, double *bytes, int64_t *compressed_po
 int pcm_assign_kernel_name(pcm_engine *e, char *buf, size_t n) {
     if (!e || !buf || n == 0) return fail(PCM_E_ARG, "bad argument");
     if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
-    const int ls = (e->d <= 3 && lloyd_slots(e) == 8) ? 8 : LSLOT;
+    const int ls = assign_ls(e);
     const bool mask = e->d <= 3 && ls == LSLOT && e->zlev == 0;
     std::snprintf(buf, n, "k_lloyd1<%s,%d,%d,%s%s>", e->dtype == PCM_F16 ? "__half" : "float", e->d, ls,
                   mask ? "true" : "false", e->zlev > 0 ? ",crowded" : "");

@@ -29,9 +29,6 @@ constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-
 #endif
 constexpr int TPB = PCM_TPB;       // assign block size
 constexpr int TILE = 32 * TPB;     // max points per tile: <= 32 per lane, 64 per shared LDS word (see AccL)
-// k_step keeps the K new centres in LDS; above 2048 (32 KB) its occupancy drops
-// to 2 blocks/CU and k_global + k_cand is faster (K = 4096, D = 4: 241 vs 439 us)
-constexpr int KSTEP_MAX = 2048;
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int TLCAP = 256;        // tile-list capacity (lists past CAPF are scanned from global memory)
 constexpr uint32_t TL_MIN = 16;   // crowded layouts: tiles of cells with longer lists (or FULL) get tile lists
@@ -62,14 +59,18 @@ struct Ctrl {
     unsigned long long neq_saved;   // stat words changed at a halted iteration (used on resume)
     unsigned long long last_changed;
     double last_shift;
-    unsigned int step_done;         // k_step: blocks finished (the last one advances `iter`)
     unsigned int ref_sel;           // candidate lists: which reference-centre buffer (cref[ref_sel]) they were built at
     double budget;                  // ... and the centre drift they tolerate (0: exact for the reference only)
     unsigned int rebuilds;          // candidate-list rebuilds of this fit (diagnostics)
     unsigned int pad1;
-    unsigned long long neq_acc;     // k_step: changed statistic words, summed over blocks (last arriver reads, resets)
-    // k_step's ~512 blocks arrive spread over ~20 us: one counter line measured as fast as two levels
-    // over 8 group lines (24.8-26 vs 27.3 us per launch), so the arrival stays single-level.
+    // k_upd: reductions over its blocks (agent-scope atomics; the last arriver
+    // reads and resets them) and the list work it hands to k_lists
+    unsigned long long u_neq;       // changed statistic words
+    unsigned long long u_dmax;      // max squared drift from the lists' reference centres (fp64 bits)
+    unsigned long long u_smax;      // max squared shift of this iteration (fp64 bits)
+    unsigned int u_empty, u_arrive;
+    unsigned int lists, pad2;       // k_lists: 0 nothing, 1 refresh the records, 2 rebuild the lists
+    double lists_dl;                // the rebuilt lists' drift budget
     // Same-address device atomics serialise at the memory side (~12 ns each, MI355X_MICROARCH.md
     // "fanin") and hold back loads queued behind them, so bulk per-wave adds are spread instead:
     // k_label: exact-inertia limbs added per block into replica lines (folded by k_inert_fold)
@@ -623,13 +624,12 @@ __global__ __launch_bounds__(256) void k_tile_list_stats(const uint4 *__restrict
 // D = 4: a coarse cell has 4^4 = 256 fine cells and a longer coarse list
 template <int D> constexpr int cand_capc() { return D >= 4 ? 1024 : CAPC; }
 #ifndef PCM_CAND_TPB
-#define PCM_CAND_TPB 512   // k_step at config 3: 25.7 vs 28.7 us (the pair passes are latency-bound)
+#define PCM_CAND_TPB 512   // round-2 fused update at config 3: 25.7 vs 28.7 us (the pair passes are latency-bound)
 #endif
 constexpr int CAND_TPB = PCM_CAND_TPB;   // threads per candidate block (one child cell per wave at a time)
 constexpr int CAND_KBITS = 4096;         // bitmap capacity (larger K: direct ballot compaction)
 constexpr int CAND_CBW = 512;            // pair path: child bitmap words (4 KB)
 constexpr int CAND_MAXCH = 64;           // pair path: children per block
-constexpr int STEP_RB = 4;               // k_step: statistics rows per thread with loads in flight together
 
 #ifdef PCM_DBG_TIMING
 __device__ unsigned long long g_dbg_t[8192][16];
@@ -666,11 +666,20 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-// C: the K centres, in global memory (k_cand) or in LDS (k_step).
+// C: the K centres, in global memory (k_cand, k_lists, k_coarse).
+// Coarse lists computed once per coarse cell (CoarseL, D = 4 layouts whose
+// coarse cells are split over many blocks): k_coarse writes them (out), the
+// child blocks read them (in) instead of each recomputing the same list.
+struct CoarseL {
+    const uint32_t *in_cnt = nullptr;   // [ncoarse] list length or FULL
+    const int32_t *in_idx = nullptr;    // [ncoarse][cand_capc] centroid ids, ascending
+    uint32_t *out_cnt = nullptr;
+    int32_t *out_idx = nullptr;
+};
 template <int D>
 __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K, uint32_t *__restrict__ fc_cnt,
                                           float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab, int BPC,
-                                          double dl = 0.0) {
+                                          double dl = 0.0, CoarseL cl = CoarseL{}) {
     constexpr int CAP = cand_capc<D>();
     const long long I = blockIdx.x / BPC;
     const int bsub = blockIdx.x % BPC;
@@ -688,7 +697,18 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     const int cpb = (nchild + BPC - 1) / BPC;
 
     // ---- 1. coarse list
-    if (g.prune) {
+    if (cl.in_cnt) {   // computed by k_coarse for this iteration's centres
+        for (int w = tid; w < CAND_CBW; w += CAND_TPB) cbits[w] = 0ull;
+        if (tid == 0) s_mp = cl.in_cnt[I];
+        __syncthreads();
+        const uint32_t m0 = s_mp;
+        if (m0 != FULL)
+            for (uint32_t l = tid; l < m0; l += CAND_TPB) {
+                const int j = cl.in_idx[(size_t)I * CAP + l];
+                pidx[l] = j;
+                prec[l] = C[j];
+            }
+    } else if (g.prune) {
         int f0[MAXD], f1[MAXD];
         for (int a = 0; a < D; ++a) {
             f0[a] = ci[a] * 4;
@@ -782,6 +802,12 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     __syncthreads();
     uint32_t mp = s_mp;
     const bool pfull = (mp == FULL);
+    if (cl.out_cnt) {   // k_coarse: publish the coarse list, no children
+        if (tid == 0) cl.out_cnt[I] = mp;
+        if (!pfull)
+            for (uint32_t l = tid; l < mp; l += CAND_TPB) cl.out_idx[(size_t)I * CAP + l] = pidx[l];
+        return;
+    }
     if (pfull) mp = (uint32_t)K;
     DBG_T(1);
     DBG_V(8, mp);
@@ -1011,22 +1037,43 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
 }
 
 // Standalone candidate lists, exact for the current centres C (drift budget 0;
-// fit start, relocation resume, final E-step, K > KSTEP_MAX): the reference
-// buffer cref[ctrl->ref_sel] := C so that k_step measures drift from C.
+// fit start, relocation resume, final E-step): the reference
+// buffer cref[ctrl->ref_sel] := C so that k_upd measures drift from C.
 template <int D>
 __global__ __launch_bounds__(CAND_TPB) void k_cand(Grid g, const float4 *__restrict__ C, int K,
                                               uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
                                               int32_t *__restrict__ fc_lab, Ctrl *__restrict__ ctrl, int gate,
-                                              int bpc, float4 *__restrict__ cref) {
+                                              int bpc, float4 *__restrict__ cref, CoarseL cl) {
     if (gate && gated(ctrl)) return;
     float4 *ref = cref + (size_t)ctrl->ref_sel * K;
     for (long long j = blockIdx.x * (long long)CAND_TPB + threadIdx.x; j < K; j += (long long)gridDim.x * CAND_TPB)
         ref[j] = C[j];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctrl->budget = 0.0;
-        if (gate) ctrl->rebuilds += 1u;   // per-iteration lists (K > KSTEP_MAX, resume)
+        if (gate) ctrl->rebuilds += 1u;   // lists rebuilt at a relocation resume
     }
-    cand_body<D>(g, C, K, fc_cnt, fc_rec, fc_lab, bpc);
+    cand_body<D>(g, C, K, fc_cnt, fc_rec, fc_lab, bpc, 0.0, cl);
+}
+
+// Coarse lists only (one block per coarse cell), for the child blocks of
+// k_cand / k_lists to read.  C: the centres the lists are for; lists: gate on
+// the k_lists work flag (the iteration path) or 0 (k_cand's callers).
+template <int D>
+__global__ __launch_bounds__(CAND_TPB) void k_coarse(Grid g, const float4 *__restrict__ C, int K,
+                                                const Ctrl *__restrict__ ctrl, int lists, uint32_t *__restrict__ cl_cnt,
+                                                int32_t *__restrict__ cl_idx) {
+    double dl = 0.0;
+    if (lists) {
+        unsigned halt = ctrl->halt;
+        unsigned mode = ctrl->lists;
+        dl = ctrl->lists_dl;
+        asm volatile("" : "+s"(halt), "+s"(mode), "+s"(dl));
+        if (halt != 0u || mode != 2u) return;   // only a rebuild needs coarse lists
+    }
+    CoarseL cl;
+    cl.out_cnt = cl_cnt;
+    cl.out_idx = cl_idx;
+    cand_body<D>(g, C, K, nullptr, nullptr, nullptr, 1, dl, cl);
 }
 
 // Candidate records refreshed to the new centres (lists still valid under the
@@ -1844,7 +1891,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         if (tid < NSUB) { okey[tid] = ~0u; omask[tid] = 0ull; }
         __syncthreads();
         // (sub-cell o, list position j) pairs: reference = a candidate nearest
-        // the sub-cell's centre (LDS atomic min of the key of k_step's children)
+        // the sub-cell's centre (LDS atomic min of the key of the candidate lists. children)
         const int np = NSUB * mm;
         for (int p = tid; p < np; p += TPB) {
             const int o = p / mm, j = p - o * mm;
@@ -2187,203 +2234,176 @@ __global__ __launch_bounds__(1024) void k_global(unsigned long long *__restrict_
     }
 }
 
-// ------------------------------------------------------------------ fused update + candidates
-// One launch per iteration for the centre update AND the next iteration's
-// candidate lists (K <= KSTEP_MAX).  Every block recomputes the K new centres
-// from the integer statistics into LDS -- deterministic, so all blocks agree
-// bit for bit -- and then either
-//  * REFRESHES the records of its cells' lists to the new centres, when every
-//    centre is still within the lists' drift budget of the reference position
-//    the lists were built at (see prunable: the lists stay exact), or
-//  * REBUILDS its cells' lists at the new centres with a new budget
-//    alpha * (this iteration's largest centre shift), capped at kappa * the
-//    smallest cell width (above that: budget 0, exact lists).
-// The decision uses maxima over all K centres computed identically in every
-// block.  The bookkeeping of k_global is spread over the blocks: each block
-// owns a slice of the statistic words (statistics-equality test against the
-// previous iteration, relocation snapshot, zeroing the next parity half) and
-// every block keeps the per-lane shift sums of the fixed tree in registers.
-// The last block to finish reduces the tree, publishes C := new centres, the
-// new reference/budget, the history, the iteration and the flags, and
-// (stats_in) zeroes the all-reduce buffer for the next accumulation.  An
-// empty cluster halts (the host relocates, then k_global + k_cand resume).
-// stats_in: the all-reduced statistics (multi-GPU) or nullptr =
-// partials[parity] (single GPU).
-#ifndef PCM_STEP_WAVES
-#define PCM_STEP_WAVES 4   // >= 4 waves/SIMD (VGPR <= 128): 4 resident 256-thread blocks per CU
-#endif
+// ------------------------------------------------------------------ centre update + candidate lists
+// One Lloyd iteration's M-step (_average_centers, _center_shift, the
+// convergence tests; _k_means_common.pyx:274-311, _kmeans.py:717-732) and the
+// next iteration's candidate lists, in two launches:
+//
+//  k_upd   one thread per centroid: its row of the (all-reduced) integer
+//          statistics -> the new centre Cn[j] (computed ONCE per iteration),
+//          the statistics-equality test against the previous iteration, the
+//          relocation snapshot `held`, zeroing of the next accumulation target,
+//          its squared shift sh[j] and drift from the lists' reference centre.
+//          Block sums/maxima go to ctrl by agent-scope atomics; the last block
+//          to arrive reduces the shift with the fixed 1024-lane tree of
+//          oracle/lloyd_ref.py shift_total, halts on an empty cluster (the host
+//          relocates, then k_global + k_cand resume), or publishes the history,
+//          flags and the list work: REFRESH the lists' records when every
+//          centre is still within the lists' drift budget of the reference
+//          position they were built at (the lists stay exact, see prunable),
+//          else REBUILD them at the new centres with budget alpha * (largest
+//          shift), capped at kappa * the smallest cell width (budget 0 above).
+//  k_lists C := Cn (and the new reference buffer when rebuilding), then the
+//          refresh or rebuild of this block's cells (cand_body / refresh_body
+//          reading the new centres from global memory).
+//
+// Hand-off inside k_upd (MI355X_MICROARCH.md, hand-off table row 1): sh[] is
+// written with sc1 stores, every storing wave drains them (vmcnt(0)) before
+// the block barrier, one lane per block adds to the arrival counter, and the
+// last arriver reads sh[] and the atomics with sc1 loads.
+constexpr int UPD_TPB = 128;
+constexpr int SHIFT_LANES = 1024;   // oracle/lloyd_ref.py SHIFT_LANES
+constexpr int UPD_LPT = SHIFT_LANES / UPD_TPB;   // tree lanes per thread of the last block
+static_assert(UPD_TPB == 128, "k_upd's last tree steps: one LDS step (h = 64), then wave shuffles");
 template <int D>
-__global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsigned long long *__restrict__ stats_in,
-                                              unsigned long long *__restrict__ partials, int K, QExp qe,
-                                              unsigned long long *__restrict__ held,
-                                              unsigned long long *__restrict__ prev, float4 *__restrict__ C,
-                                              float4 *__restrict__ cref,
-                                              unsigned long long *__restrict__ hist_changed,
-                                              double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl,
-                                              uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
-                                              int32_t *__restrict__ fc_lab, int bpc, double alpha, double dl_cap) {
-    static_assert(1024 % CAND_TPB == 0 && CAND_TPB >= 128, "shift tree: 1024 lanes over the block");
-    constexpr int NU = 1024 / CAND_TPB;   // shift-tree lanes L = tid + CAND_TPB * u per thread
+__global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict__ stats_in,
+                                                 unsigned long long *__restrict__ partials, int K, QExp qe,
+                                                 unsigned long long *__restrict__ held,
+                                                 unsigned long long *__restrict__ prev, const float4 *__restrict__ C,
+                                                 float4 *__restrict__ Cn, const float4 *__restrict__ cref,
+                                                 double *__restrict__ sh, unsigned long long *__restrict__ hist_changed,
+                                                 double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl, double alpha,
+                                                 double dl_cap) {
     // the gate flags and the control words this launch reads, in one memory latency
     unsigned gate = ctrl->halt | ctrl->done;
     unsigned par = ctrl->iter & 1u;
     unsigned sel = ctrl->ref_sel;
-    double budget = ctrl->budget;
-    asm volatile("" : "+s"(gate), "+s"(par), "+s"(sel), "+s"(budget));   // keep the loads above the exit
+    asm volatile("" : "+s"(gate), "+s"(par), "+s"(sel));   // keep the loads above the exit
     if (gate != 0u) return;
-    DBG_T(0);
-    extern __shared__ __attribute__((aligned(16))) float4 cn[];   // [K]
-    __shared__ unsigned s_empty, s_last;
-    __shared__ unsigned long long s_neq;
-    __shared__ double s_tree[CAND_TPB];
-    __shared__ double s_dmax[CAND_TPB / 64], s_smax[CAND_TPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = K * (D + 1);
-    const unsigned long long *src = stats_in ? stats_in : partials + (size_t)par * n;
-    const float4 *ref = cref + (size_t)sel * K;
-    if (tid == 0) { s_empty = 0; s_neq = 0ull; }
-    __syncthreads();
-    unsigned ne = 0;
-    double dmax = 0.0, smax = 0.0;   // squared drift from the reference / squared shift this iteration
-    // shift of centre j = tid + CAND_TPB * v added to tree lane L = j mod 1024,
-    // i.e. tacc[v % NU], in ascending j (the sequential per-lane sums of
-    // oracle/lloyd_ref.py shift_total); every block holds them, the last
-    // arriver reduces its own copy with the fixed tree.
-    double tacc[NU];
+    const int j = blockIdx.x * UPD_TPB + tid;
+    unsigned long long *src = stats_in ? stats_in : partials + (size_t)par * n;
+    unsigned long long neq = 0ull;
+    unsigned ne = 0u;
+    double dr = 0.0, ds = 0.0;
+    if (j < K) {
+        const size_t o = (size_t)j * (D + 1);
+        unsigned long long row[D + 1], pv[D + 1];
 #pragma unroll
-    for (int u = 0; u < NU; ++u) tacc[u] = 0.0;
-    // rows j = tid + CAND_TPB * (j0 + u): STEP_RB rows' loads are all issued before any is used
-    constexpr int RB = STEP_RB;
-    static_assert(RB % NU == 0, "row batches map onto tree lanes");
-    for (int j0 = 0; j0 * CAND_TPB < K; j0 += RB) {
-        unsigned long long row[RB][D + 1];
-        float4 rj[RB], oj[RB];
+        for (int a = 0; a <= D; ++a) { row[a] = src[o + a]; pv[a] = prev[o + a]; }
+        const float4 rj = cref[(size_t)sel * K + j], oj = C[j];
+        unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
 #pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const int j = tid + CAND_TPB * (j0 + u);
-            const int jj = j < K ? j : K - 1;
-#pragma unroll
-            for (int a = 0; a <= D; ++a) row[u][a] = src[(size_t)jj * (D + 1) + a];
-            rj[u] = ref[jj];
-            oj[u] = C[jj];
+        for (int a = 0; a <= D; ++a) {
+            neq += (row[a] != pv[a]) ? 1ull : 0ull;   // convergence: raw statistics equal the previous ones
+            prev[o + a] = row[a];
+            held[o + a] = row[a];                     // the relocation snapshot, should this iteration halt
+            pnext[o + a] = 0ull;                      // the next accumulation starts from zero
         }
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const int j = tid + CAND_TPB * (j0 + u);
-            if (j >= K) break;
-            const unsigned long long c = row[u][D];
-            float out[4] = {0.f, 0.f, 0.f, 0.f};
-            if (c > 0) {
-#pragma unroll
-                for (int a = 0; a < D; ++a) {
-                    const double m = ((double)(long long)row[u][a] * __builtin_ldexp(1.0, -qe.q[a])) / (double)c;
-                    out[a] = (float)m;
-                }
-            } else {
-                ++ne;
-            }
-            const float4 v = make_float4(out[0], out[1], out[2], out[3]);
-            cn[j] = v;
-            double dr = 0.0, ds = 0.0;
+        const unsigned long long c = row[D];
+        float out[4] = {0.f, 0.f, 0.f, 0.f};
+        if (c > 0) {
 #pragma unroll
             for (int a = 0; a < D; ++a) {
-                const double e1 = (double)comp(v, a) - (double)comp(rj[u], a);
-                const double e2 = (double)comp(v, a) - (double)comp(oj[u], a);
-                dr += e1 * e1;
-                ds += e2 * e2;
+                const double m = ((double)(long long)row[a] * __builtin_ldexp(1.0, -qe.q[a])) / (double)c;
+                out[a] = (float)m;
             }
-            dmax = fmax(dmax, dr);
-            smax = fmax(smax, ds);
-            tacc[u % NU] = tacc[u % NU] + ds;   // j0 is a multiple of RB, RB of NU
+        } else {
+            ne = 1u;
         }
+        const float4 v = make_float4(out[0], out[1], out[2], out[3]);
+        Cn[j] = v;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const double e1 = (double)comp(v, a) - (double)comp(rj, a);
+            const double e2 = (double)comp(v, a) - (double)comp(oj, a);
+            dr += e1 * e1;
+            ds += e2 * e2;
+        }
+        __hip_atomic_store(sh + j, ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (j == 0) {
+        held[n] = 0ull;
+        if (stats_in) stats_in[n] = 0ull;
     }
     for (int o = 32; o > 0; o >>= 1) {
-        dmax = fmax(dmax, __shfl_xor(dmax, o));
-        smax = fmax(smax, __shfl_xor(smax, o));
+        neq += __shfl_xor(neq, o);
+        ne += __shfl_xor(ne, o);
+        dr = fmax(dr, __shfl_xor(dr, o));
+        ds = fmax(ds, __shfl_xor(ds, o));
     }
-    if (lane == 0) { s_dmax[wv] = dmax; s_smax[wv] = smax; }
-    if (ne) atomicAdd(&s_empty, ne);
-    __syncthreads();
-    DBG_T(6);
-    // This block's slice of the statistic words: convergence (sklearn: labels
-    // equal) as raw statistics equal to the previous iteration's, the relocation
-    // snapshot, and (single GPU) zeroing the other parity half for the next
-    // accumulation.  The changed-word count reaches the last arriver through
-    // ctrl->neq_acc.
-    {
-        const bool halting = s_empty > 0;
-        unsigned long long *pnext = partials + (size_t)(par ^ 1u) * n;
-        for (int i = blockIdx.x * CAND_TPB + tid; i < n; i += gridDim.x * CAND_TPB) {
-            const unsigned long long v = src[i], pv = prev[i];
-            if (v != pv) atomicAdd(&s_neq, 1ull);
-            prev[i] = v;
-            if (!stats_in) pnext[i] = 0ull;
-            if (halting) held[i] = v;
-        }
-        if (halting && blockIdx.x == 0 && tid == 0) held[n] = 0ull;
-    }
-    const bool halt = s_empty > 0;
-    dmax = s_dmax[0];
-    smax = s_smax[0];
-    for (int w = 1; w < CAND_TPB / 64; ++w) { dmax = fmax(dmax, s_dmax[w]); smax = fmax(smax, s_smax[w]); }
-    const double slack = 1.0 + 9.094947017729282e-13;   // 1 + 2^-40: fp64 rounding of the drift norms
-    const bool rebuild = !(sqrt(dmax) * slack <= budget);
-    double dl_new = alpha * sqrt(smax) * slack;
-    if (!(dl_new <= dl_cap)) dl_new = 0.0;
-    if (!halt) {
-        if (rebuild) cand_body<D>(g, cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new);
-        else refresh_body<D>(g, cn, fc_cnt, fc_rec, fc_lab, bpc);
-    }
-    DBG_T(3);
-    // Arrival.  Every block has read ctrl (parity, reference, budget) and C
-    // before any block can observe the final count, so only the last block
-    // publishes.  The only value written in this launch and read later in it
-    // is neq_acc (an L2 atomic drained by s_waitcnt before the arrival, read
-    // with an agent-scope load by the last arriver), so the arrival needs no
-    // L2 write-back fence (MI355X_MICROARCH.md hand-off row 1).
+    __shared__ unsigned long long s_neq[UPD_TPB / 64];
+    __shared__ unsigned s_ne[UPD_TPB / 64];
+    __shared__ double s_dr[UPD_TPB / 64], s_ds[UPD_TPB / 64];
+    __shared__ unsigned s_last;
+    if (lane == 0) { s_neq[wv] = neq; s_ne[wv] = ne; s_dr[wv] = dr; s_ds[wv] = ds; }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores of sh
     __syncthreads();
     if (tid == 0) {
-        if (s_neq) __hip_atomic_fetch_add(&ctrl->neq_acc, s_neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int w = 1; w < UPD_TPB / 64; ++w) {
+            neq += s_neq[w]; ne += s_ne[w]; dr = fmax(dr, s_dr[w]); ds = fmax(ds, s_ds[w]);
+        }
+        if (neq) __hip_atomic_fetch_add(&ctrl->u_neq, neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ne) __hip_atomic_fetch_add(&ctrl->u_empty, ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // non-negative doubles order like their bit patterns
+        __hip_atomic_fetch_max(&ctrl->u_dmax, (unsigned long long)__double_as_longlong(dr), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(&ctrl->u_smax, (unsigned long long)__double_as_longlong(ds), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prior = __hip_atomic_fetch_add(&ctrl->step_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (prior == gridDim.x - 1) ? 1u : 0u;
     }
     __syncthreads();
     if (!s_last) return;
-    const unsigned long long changed = __hip_atomic_load(&ctrl->neq_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (halt) {   // empty cluster: the host relocates, then k_global + k_cand resume
+    // ---- the last block: every other block's stores and atomics have landed
+    const unsigned long long changed = __hip_atomic_load(&ctrl->u_neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned n_empty = __hip_atomic_load(&ctrl->u_empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double dmax = __longlong_as_double(
+        (long long)__hip_atomic_load(&ctrl->u_dmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const double smax = __longlong_as_double(
+        (long long)__hip_atomic_load(&ctrl->u_smax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();   // every lane has read the totals before lane 0 resets them
+    if (tid == 0) {
+        __hip_atomic_store(&ctrl->u_neq, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->u_empty, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->u_dmax, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->u_smax, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->u_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (n_empty > 0u) {   // empty cluster: the host relocates, then k_global + k_cand resume
         if (tid == 0) {
-            ctrl->step_done = 0u;
-            ctrl->neq_acc = 0ull;
-            ctrl->n_empty = s_empty;
+            ctrl->n_empty = n_empty;
             ctrl->neq_saved = changed;
+            ctrl->lists = 0u;
             ctrl->halt = 1u;
         }
         return;
     }
-    // total shift: the fixed tree of k_global / oracle shift_total over 1024 lanes
+    // total shift: lane L sums sh[L + 1024 r] in ascending r, then the halving tree
+    double v[UPD_LPT];
 #pragma unroll
-    for (int st = 512, h = NU / 2; st >= CAND_TPB; st >>= 1, h >>= 1)
+    for (int u = 0; u < UPD_LPT; ++u) v[u] = 0.0;
+    for (int r = 0; r * SHIFT_LANES < K; ++r)
 #pragma unroll
-        for (int u = 0; u < h; ++u) tacc[u] = tacc[u] + tacc[u + h];
-    s_tree[tid] = tacc[0];
-    for (int j = tid; j < K; j += CAND_TPB) C[j] = cn[j];
-    if (rebuild) {
-        float4 *nref = cref + (size_t)(sel ^ 1u) * K;
-        for (int j = tid; j < K; j += CAND_TPB) nref[j] = cn[j];
-    }
-    if (stats_in)   // every block has read the all-reduced statistics: zero them for the next accumulation
-        for (int i = tid; i < n + 1; i += CAND_TPB) stats_in[i] = 0ull;
+        for (int u = 0; u < UPD_LPT; ++u) {
+            const int idx = r * SHIFT_LANES + tid + UPD_TPB * u;
+            if (idx < K) v[u] = v[u] + __hip_atomic_load(sh + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+    for (int h = UPD_LPT / 2; h >= 1; h >>= 1)   // lanes L and L + UPD_TPB * h live in this thread
+#pragma unroll
+        for (int u = 0; u < h; ++u) v[u] = v[u] + v[u + h];
+    __shared__ double s_tree[UPD_TPB];
+    s_tree[tid] = v[0];
     __syncthreads();
-    for (int st = CAND_TPB / 2; st >= 64; st >>= 1) {
-        if (tid < st) s_tree[tid] = s_tree[tid] + s_tree[tid + st];
-        __syncthreads();
-    }
     if (wv == 0) {
-        double v = s_tree[lane];
-        for (int st = 32; st > 0; st >>= 1) v = v + __shfl_down(v, st);   // lane t: v_t + v_{t+st}
+        double x = s_tree[lane];
+        x = x + s_tree[lane + 64];
+        for (int st = 32; st > 0; st >>= 1) x = x + __shfl_down(x, st);   // lane t: x_t + x_{t+st}
         if (lane == 0) {
-            const double shift = v;
+            const double shift = x;
             const uint32_t it = ctrl->iter;
             if (it < ctrl->max_iter) {
                 hist_changed[it] = changed;
@@ -2391,14 +2411,19 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
             }
             ctrl->last_changed = changed;
             ctrl->last_shift = shift;
-            ctrl->step_done = 0u;
-            ctrl->neq_acc = 0ull;
             ctrl->resume = 0u;
+            const double slack = 1.0 + 9.094947017729282e-13;   // 1 + 2^-40: fp64 rounding of the drift norms
+            const double budget = ctrl->budget;
+            const bool rebuild = !(sqrt(dmax) * slack <= budget);
+            double dl_new = alpha * sqrt(smax) * slack;
+            if (!(dl_new <= dl_cap)) dl_new = 0.0;
             if (rebuild) {
                 ctrl->ref_sel = sel ^ 1u;
                 ctrl->budget = dl_new;
                 ctrl->rebuilds += 1u;
             }
+            ctrl->lists = rebuild ? 2u : 1u;
+            ctrl->lists_dl = rebuild ? dl_new : budget;
             uint32_t done = 0;
             if (changed == 0ull) done = 1u;
             else if (shift <= ctrl->tol) done = 2u;
@@ -2407,7 +2432,32 @@ __global__ __launch_bounds__(CAND_TPB, PCM_STEP_WAVES) void k_step(Grid g, unsig
             ctrl->iter = it + 1;
         }
     }
-    DBG_T(7);
+}
+
+// C := Cn (the centres k_upd published) and the next iteration's candidate
+// lists: a rebuild at Cn with the published budget (the new reference buffer
+// cref[ref_sel] := Cn) or a refresh of the records.  Runs after a completed
+// k_upd: halted iterations leave C untouched (the relocation needs the old
+// centres); queued no-op launches after convergence repeat the same copy and
+// lists (idempotent).
+template <int D>
+__global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__restrict__ Cn, float4 *__restrict__ C,
+                                                    float4 *__restrict__ cref, int K, const Ctrl *__restrict__ ctrl,
+                                                    uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
+                                                    int32_t *__restrict__ fc_lab, int bpc, CoarseL cl) {
+    unsigned halt = ctrl->halt;
+    unsigned mode = ctrl->lists;
+    unsigned sel = ctrl->ref_sel;
+    double dl = ctrl->lists_dl;
+    asm volatile("" : "+s"(halt), "+s"(mode), "+s"(sel), "+s"(dl));
+    if (halt != 0u || mode == 0u) return;
+    for (int j = blockIdx.x * CAND_TPB + threadIdx.x; j < K; j += gridDim.x * CAND_TPB) {
+        const float4 c = Cn[j];
+        C[j] = c;
+        if (mode == 2u) cref[(size_t)sel * K + j] = c;
+    }
+    if (mode == 2u) cand_body<D>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+    else refresh_body<D>(g, Cn, fc_cnt, fc_rec, fc_lab, bpc);
 }
 
 // ------------------------------------------------------------------ relocation

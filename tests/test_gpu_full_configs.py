@@ -158,7 +158,9 @@ def test_config3_bench_length_fit_matches_bruteforce(gpu):
     nbad = int((lab_bf != res.labels).sum())
     assert nbad == 0, f"{nbad} of {n} pruned labels differ from the brute-force E-step"
     # exact statistics of the engine's labels (int64 fixed point, order independent)
-    xq = torch.ldexp(X, torch.as_tensor(q, device="cuda").float()).trunc().to(torch.int64)
+    # exact power-of-two scales (torch.ldexp goes through pow(2, q), which is not exact on the device)
+    scale = torch.tensor([2.0 ** int(qa) for qa in q], dtype=torch.float32, device="cuda")
+    xq = (X * scale).trunc().to(torch.int64)
     mine = torch.zeros((k, d + 1), dtype=torch.int64, device="cuda")
     mine[:, :d].index_add_(0, res.labels.long(), xq)
     mine[:, d] = torch.bincount(res.labels.long(), minlength=k)
