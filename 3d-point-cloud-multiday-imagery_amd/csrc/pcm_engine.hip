@@ -91,6 +91,7 @@ struct pcm_engine {
     float4 *C = nullptr, *Cn = nullptr;
     float4 *cref = nullptr;                    // [2][K] reference centres of the candidate lists (k_upd / k_lists)
     double *shbuf = nullptr;                   // [K] squared centre shifts of one iteration (k_upd's shift tree)
+    UpdPart *upart = nullptr;                  // [ceil(K / UPD_TPB)] k_upd's per-block records
     uint32_t *cl_cnt = nullptr;                // [ncoarse] coarse candidate lists (k_coarse; split layouts)
     int32_t *cl_idx = nullptr;                 // [ncoarse][cand_capc]
     size_t cap_clc = 0, cap_cli = 0;
@@ -413,6 +414,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->Cn, (size_t)k * sizeof(float4));
     err = err ? err : hipMalloc(&e->cref, (size_t)2 * k * sizeof(float4));
     err = err ? err : hipMalloc(&e->shbuf, (size_t)k * sizeof(double));
+    err = err ? err : hipMalloc(&e->upart, (size_t)blocks_for(k, UPD_TPB) * sizeof(UpdPart));
     err = err ? err : hipMalloc(&e->prev, nstat * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->partials, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->stats_own, nstat * sizeof(unsigned long long));
@@ -448,7 +450,7 @@ int pcm_engine_destroy(pcm_engine *e) {
         for (int j = 0; j < 4; ++j)
             if (e->ev[i][j]) (void)hipEventDestroy(e->ev[i][j]);
     free_buffers(e);
-    void *ps[] = {e->C, e->Cn, e->cref, e->shbuf, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
+    void *ps[] = {e->C, e->Cn, e->cref, e->shbuf, e->upart, e->prev, e->partials, e->stats_own, e->held, e->hist_changed, e->hist_shift, e->ctrl,
                   e->bbox_part, e->nonfinite, e->bbox_out, e->cand_stats, e->rank_buf, e->empty_idx, e->ntiles_dev,
                   e->grows, e->zpts};
     for (void *p : ps)
@@ -771,10 +773,18 @@ static int cand_bpc(const pcm_engine *e) {
     return (int)std::max(1LL, std::min(8LL, b));
 }
 
-// Coarse cells split over many blocks (D = 4: 256 children, 32 blocks each)
-// get their coarse list computed once, by k_coarse, instead of once per block
-// (config-5 shard: the same K = 4096 pruning pass 32 times per coarse cell).
-static bool split_coarse(const pcm_engine *e) { return e->g.prune && cand_bpc(e) >= 8; }
+// D = 4 coarse cells hold 4^4 = 256 fine cells and long lists: their lists are
+// built in three levels -- k_coarse (one block per coarse cell, all K centres,
+// once) -> one block per mid cell (2^4 fine cells) refining its coarse parent's
+// list -> its 16 fine cells (k_cand / k_lists with FC = 2) -- instead of 32
+// blocks per coarse cell each recomputing the coarse list and then pruning it
+// per fine cell (config-5 shard: 252 us of k_cand per iteration).
+static bool split_coarse(const pcm_engine *e) { return e->g.prune && e->d >= 4; }
+static long long n_mid(const pcm_engine *e) {
+    long long m = 1;
+    for (int a = 0; a < e->d; ++a) m *= (e->g.G[a] + 1) / 2;
+    return m;
+}
 
 // coarse-list storage of the current layout (split layouts only)
 static int ensure_coarse(pcm_engine *e) {
@@ -789,16 +799,20 @@ static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
         const int bpc = cand_bpc(e);
-        CoarseL cl;
         if (split_coarse(e)) {
             if (int rc = ensure_coarse(e)) return rc;
             k_coarse<D><<<(int)e->g.ncoarse, CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->ctrl, 0, e->cl_cnt, e->cl_idx);
             LAUNCHCHK();
+            CoarseL cl;
             cl.in_cnt = e->cl_cnt;
             cl.in_idx = e->cl_idx;
+            k_cand<D, 2><<<(int)n_mid(e), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab, e->ctrl,
+                                                             gate, 1, e->cref, cl);
+            LAUNCHCHK();
+            return 0;
         }
         k_cand<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, 0, s>>>(e->g, e->C, e->k, e->fc_cnt, e->fc_rec, e->fc_lab,
-                                                                 e->ctrl, gate, bpc, e->cref, cl);
+                                                                 e->ctrl, gate, bpc, e->cref, CoarseL{});
         LAUNCHCHK();
         return 0;
     });
@@ -842,10 +856,13 @@ static int lloyd_slots(const pcm_engine *e) {
     return (e->g.prune && (double)e->g.ncells >= 8.0 * e->k * share) ? 8 : LSLOT;
 }
 
-// Lane slots of the launched k_lloyd1: 8 on fine grids at D <= 3 (and at D = 4
-// with PCM_D4_LS8=1, a tuning switch), else LSLOT.
+// Lane slots of the launched k_lloyd1: 8 on fine grids, else LSLOT.  D = 4
+// (config 5: lists of ~8, up to 27) takes 8 slots since the slot map gives them
+// to the candidates nearest each tile (k_lloyd1): 11.5 instead of 21.8 KB of
+// LDS words per block, 5 instead of 3 waves per SIMD -- config-5 shard 404 ->
+// 325 us per launch, 8-way slab 270 -> 220 us (round 4; PCM_D4_LS8=0 restores 16).
 static int assign_ls(const pcm_engine *e) {
-    static const bool d4_ls8 = [] { const char *v = std::getenv("PCM_D4_LS8"); return v && std::atoi(v); }();
+    static const bool d4_ls8 = [] { const char *v = std::getenv("PCM_D4_LS8"); return !v || std::atoi(v); }();
     return ((e->d <= 3 || d4_ls8) && lloyd_slots(e) == 8) ? 8 : LSLOT;
 }
 
@@ -872,6 +889,7 @@ static LloydArgs lloyd_args(pcm_engine *e) {
     A.tl_cnt = e->zlev > 0 ? e->tl_cnt : nullptr;
     A.tl_rec = e->zlev > 0 ? e->tl_rec : nullptr;
     A.tl_lab = e->zlev > 0 ? e->tl_lab : nullptr;
+    A.tbox = e->zlev > 0 ? e->tbox : nullptr;
     return A;
 }
 
@@ -1001,19 +1019,23 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
                 if (e->g.ext[a] > 0 && (wmin == 0.0 || e->g.w[a] < wmin)) wmin = e->g.w[a];
             k_upd<D><<<blocks_for(e->k, UPD_TPB), UPD_TPB, 0, s>>>(
                 from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->Cn, e->cref,
-                e->shbuf, e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin);
+                e->shbuf, e->upart, e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin);
             LAUNCHCHK();
-            const int bpc = cand_bpc(e);
-            CoarseL cl;
             if (split_coarse(e)) {
                 if (int rc = ensure_coarse(e)) return rc;
                 k_coarse<D><<<(int)e->g.ncoarse, CAND_TPB, 0, s>>>(e->g, e->Cn, e->k, e->ctrl, 1, e->cl_cnt, e->cl_idx);
                 LAUNCHCHK();
+                CoarseL cl;
                 cl.in_cnt = e->cl_cnt;
                 cl.in_idx = e->cl_idx;
+                k_lists<D, 2><<<(int)n_mid(e), CAND_TPB, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl, e->fc_cnt,
+                                                                  e->fc_rec, e->fc_lab, 1, cl);
+            } else {
+                const int bpc = cand_bpc(e);
+                k_lists<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl,
+                                                                           e->fc_cnt, e->fc_rec, e->fc_lab, bpc,
+                                                                           CoarseL{});
             }
-            k_lists<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl,
-                                                                       e->fc_cnt, e->fc_rec, e->fc_lab, bpc, cl);
             LAUNCHCHK();
             return 0;
         }

@@ -63,12 +63,9 @@ struct Ctrl {
     double budget;                  // ... and the centre drift they tolerate (0: exact for the reference only)
     unsigned int rebuilds;          // candidate-list rebuilds of this fit (diagnostics)
     unsigned int pad1;
-    // k_upd: reductions over its blocks (agent-scope atomics; the last arriver
-    // reads and resets them) and the list work it hands to k_lists
-    unsigned long long u_neq;       // changed statistic words
-    unsigned long long u_dmax;      // max squared drift from the lists' reference centres (fp64 bits)
-    unsigned long long u_smax;      // max squared shift of this iteration (fp64 bits)
-    unsigned int u_empty, u_arrive;
+    // k_upd: arrival counter of its blocks (the last one reduces their records and
+    // resets it) and the list work it hands to k_lists
+    unsigned int u_arrive, pad3;
     unsigned int lists, pad2;       // k_lists: 0 nothing, 1 refresh the records, 2 rebuild the lists
     double lists_dl;                // the rebuilt lists' drift budget
     // Same-address device atomics serialise at the memory side (~12 ns each, MI355X_MICROARCH.md
@@ -667,37 +664,54 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 }
 
 // C: the K centres, in global memory (k_cand, k_lists, k_coarse).
-// Coarse lists computed once per coarse cell (CoarseL, D = 4 layouts whose
-// coarse cells are split over many blocks): k_coarse writes them (out), the
-// child blocks read them (in) instead of each recomputing the same list.
+// Coarse lists computed once per coarse cell (CoarseL, D = 4 layouts): k_coarse
+// writes them (out); the blocks of the next level read them (in).
 struct CoarseL {
     const uint32_t *in_cnt = nullptr;   // [ncoarse] list length or FULL
     const int32_t *in_idx = nullptr;    // [ncoarse][cand_capc] centroid ids, ascending
     uint32_t *out_cnt = nullptr;
     int32_t *out_idx = nullptr;
 };
-template <int D>
+// FC: fine cells per axis of the block's cell.  FC = 4: a coarse cell (4^D
+// children) whose list is computed from all K centres (or read from k_coarse);
+// FC = 2: a mid cell (2^D children, D = 4 layouts) whose list REFINES its
+// coarse parent's k_coarse list -- the same exact test against the mid box --
+// so the fine lists prune ~2^D-times shorter lists than the coarse ones.
+template <int D, int FC = 4>
 __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K, uint32_t *__restrict__ fc_cnt,
                                           float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab, int BPC,
                                           double dl = 0.0, CoarseL cl = CoarseL{}) {
+    static_assert(FC == 4 || FC == 2, "children per axis");
     constexpr int CAP = cand_capc<D>();
+    constexpr int FS = FC == 4 ? 2 : 1;   // log2(FC)
     const long long I = blockIdx.x / BPC;
     const int bsub = blockIdx.x % BPC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     __shared__ float4 prec[CAP];
     __shared__ int pidx[CAP];
+    __shared__ int sidx[FC == 2 ? CAP : 1];   // refine: the coarse parent's list
     __shared__ unsigned long long kbits[CAND_KBITS / 64];
     __shared__ unsigned long long rkey;
-    __shared__ uint32_t s_mp;
+    __shared__ uint32_t s_mp, s_np;
     __shared__ unsigned long long cbits[CAND_CBW];   // pair path: per-child keep bitmaps over the coarse list
     int ci[MAXD];
-    decode(I, g.GC, D, ci);
+    long long Ipar = I;   // the coarse cell whose k_coarse list this block reads
+    if (FC == 4) {
+        decode(I, g.GC, D, ci);
+    } else {
+        int GM[MAXD], pc[MAXD];
+        for (int a = 0; a < MAXD; ++a) GM[a] = a < D ? (g.G[a] + 1) / 2 : 1;
+        decode(I, GM, D, ci);
+        for (int a = 0; a < D; ++a) pc[a] = ci[a] / 2;
+        Ipar = encode(pc, g.GC, D);
+    }
     int nchild = 1;
-    for (int a = 0; a < D; ++a) nchild *= 4;
+    for (int a = 0; a < D; ++a) nchild *= FC;
     const int cpb = (nchild + BPC - 1) / BPC;
+    const bool refine = FC == 2 && cl.in_cnt != nullptr;
 
-    // ---- 1. coarse list
-    if (cl.in_cnt) {   // computed by k_coarse for this iteration's centres
+    // ---- 1. this block's cell list
+    if (cl.in_cnt && !refine) {   // computed by k_coarse for this iteration's centres
         for (int w = tid; w < CAND_CBW; w += CAND_TPB) cbits[w] = 0ull;
         if (tid == 0) s_mp = cl.in_cnt[I];
         __syncthreads();
@@ -711,12 +725,26 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     } else if (g.prune) {
         int f0[MAXD], f1[MAXD];
         for (int a = 0; a < D; ++a) {
-            f0[a] = ci[a] * 4;
-            f1[a] = min(f0[a] + 4, g.G[a]) - 1;
+            f0[a] = ci[a] * FC;
+            f1[a] = min(f0[a] + FC, g.G[a]) - 1;
         }
         double blo[MAXD], bhi[MAXD];
         cell_box<D>(g, f0, f1, blo, bhi);
-        const bool bitmap = K <= CAND_KBITS;
+        // source candidates: every centre, or (refine) the coarse parent's list
+        int nsrc = K;
+        bool from_list = false;
+        if (refine) {
+            if (tid == 0) s_np = cl.in_cnt[Ipar];
+            __syncthreads();
+            const uint32_t m0 = s_np;
+            if (m0 != FULL) {
+                nsrc = (int)m0;
+                from_list = true;
+                for (int l = tid; l < nsrc; l += CAND_TPB) sidx[l] = cl.in_idx[(size_t)Ipar * CAP + l];
+            }
+        }
+        auto src = [&](int p) -> int { return from_list ? sidx[p] : p; };
+        const bool bitmap = nsrc <= CAND_KBITS;
         if (tid == 0) rkey = ~0ull;
         if (bitmap)
             for (int w = tid; w < CAND_KBITS / 64; w += CAND_TPB) kbits[w] = 0ull;
@@ -727,7 +755,8 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         // j's wave-local rank -> per-wave DPP minimum, then one LDS atomic per wave
         uint32_t best = ~0u;
         int bjj = 0;
-        for (int j = tid; j < K; j += CAND_TPB) {
+        for (int p = tid; p < nsrc; p += CAND_TPB) {
+            const int j = src(p);
             const float m = (float)maxdist<D>(blo, bhi, C[j]);
             if (__float_as_uint(m) < best) { best = __float_as_uint(m); bjj = j; }
         }
@@ -739,20 +768,21 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         const float4 r = C[(int)min((unsigned long long)(K - 1), rkey & 0xFFFFFFFFull)];
         const double mr = dl > 0.0 ? sqrt(maxdist<D>(blo, bhi, r)) : 0.0;
         if (bitmap) {
-            // a wave's 64 consecutive centres fill one bitmap word: a ballot and a
-            // plain store (no 64-way contended LDS atomic)
-            for (int j0 = 0; j0 < K; j0 += CAND_TPB) {
-                const int j = j0 + tid;
-                const bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r, dl, mr);
+            // a wave's 64 consecutive source positions fill one bitmap word: a
+            // ballot and a plain store (no 64-way contended LDS atomic)
+            for (int p0 = 0; p0 < nsrc; p0 += CAND_TPB) {
+                const int p = p0 + tid;
+                const bool keep = p < nsrc && !prunable<D>(blo, bhi, C[src(p < nsrc ? p : 0)], r, dl, mr);
                 const unsigned long long bal = __ballot(keep);
-                if (lane == 0 && j0 + wv * 64 < K) kbits[(j0 >> 6) + wv] = bal;
+                if (lane == 0 && p0 + wv * 64 < nsrc) kbits[(p0 >> 6) + wv] = bal;
             }
             __syncthreads();
             DBG_T(5);
-            // ordered compaction: word prefix counts by one wave-wide scan, then
-            // every wave compacts the words w = wv (mod waves) in parallel
+            // ordered compaction (ascending source position = ascending centroid
+            // index): word prefix counts by one wave-wide scan, then every wave
+            // compacts the words w = wv (mod waves) in parallel
             __shared__ uint32_t wpre[CAND_KBITS / 64];
-            const int nwk = (K + 63) / 64;   // <= 64
+            const int nwk = (nsrc + 63) / 64;   // <= 64
             if (wv == 0) {
                 const uint32_t c = lane < nwk ? (uint32_t)__popcll(kbits[lane]) : 0u;
                 uint32_t x = c;
@@ -768,8 +798,8 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
             for (int w = wv; w < nwk; w += CAND_TPB / 64) {
                 const unsigned long long word = kbits[w];
                 const uint32_t pos = wpre[w] + __popcll(word & ((1ull << lane) - 1ull));
-                const int j = w * 64 + lane;
                 if (((word >> lane) & 1ull) && pos < (uint32_t)CAP) {
+                    const int j = src(w * 64 + lane);
                     prec[pos] = C[j];
                     pidx[pos] = j;
                 }
@@ -778,9 +808,10 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
             // large K: ordered compaction by ballots (one barrier pair per CAND_TPB centres)
             __shared__ uint32_t wcnt[CAND_TPB / 64];
             uint32_t total = 0;
-            for (int base = 0; base < K; base += CAND_TPB) {
-                const int j = base + tid;
-                const bool keep = j < K && !prunable<D>(blo, bhi, C[j < K ? j : 0], r, dl, mr);
+            for (int base = 0; base < nsrc; base += CAND_TPB) {
+                const int p = base + tid;
+                const int j = src(p < nsrc ? p : 0);
+                const bool keep = p < nsrc && !prunable<D>(blo, bhi, C[j], r, dl, mr);
                 const unsigned long long bal = __ballot(keep);
                 if (lane == 0) wcnt[wv] = __popcll(bal);
                 __syncthreads();
@@ -812,13 +843,15 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     DBG_T(1);
     DBG_V(8, mp);
 
-    // ---- 2. children (F = 4 per axis) of this block: c0 .. c1-1
+    // ---- 2. children (FC per axis) of this block: c0 .. c1-1
     const int c0 = bsub * cpb, c1 = min(nchild, (bsub + 1) * cpb);
     const int nwc = (int)((mp + 63u) / 64u);   // bitmap words per child
     // pair path when each wave would otherwise walk >= 8 children one after the
     // other (100M: 64 children per block, 15 -> 9.6 us); with few children per
     // block (12.5M shard: 8) the wave path's two chains per wave are shorter
-    if (!pfull && (c1 - c0) >= 2 * CAND_TPB / 16 && (c1 - c0) <= CAND_MAXCH && (c1 - c0) * nwc <= CAND_CBW) {
+    // (mid blocks, FC = 2: 16 children over lists of tens to hundreds: the pair path too)
+    if (!pfull && ((c1 - c0) >= 2 * CAND_TPB / 16 || FC == 2) && (c1 - c0) <= CAND_MAXCH &&
+        (c1 - c0) * nwc <= CAND_CBW) {
         // Pair path: one thread per (child, coarse-list position) in three
         // block-wide passes -- (A) reference = a parent candidate nearest the
         // child's centre (LDS atomic min of the key of the wave path below),
@@ -839,8 +872,8 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
             int f[MAXD];
             bool inside = true;
 #pragma unroll
-            for (int a = D - 1, t = c0 + ch; a >= 0; --a, t >>= 2) {
-                f[a] = ci[a] * 4 + (t & 3);
+            for (int a = D - 1, t = c0 + ch; a >= 0; --a, t >>= FS) {
+                f[a] = ci[a] * FC + (t & (FC - 1));
                 inside &= f[a] < g.G[a];
             }
             double blo[MAXD], bhi[MAXD];
@@ -959,8 +992,8 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
             int f[MAXD];
             bool inside = true;
 #pragma unroll
-            for (int a = D - 1, t = ch; a >= 0; --a, t >>= 2) {
-                f[a] = ci[a] * 4 + (t & 3);
+            for (int a = D - 1, t = ch; a >= 0; --a, t >>= FS) {
+                f[a] = ci[a] * FC + (t & (FC - 1));
                 inside &= f[a] < g.G[a];
             }
             if (!inside) continue;   // wave-uniform
@@ -1039,7 +1072,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
 // Standalone candidate lists, exact for the current centres C (drift budget 0;
 // fit start, relocation resume, final E-step): the reference
 // buffer cref[ctrl->ref_sel] := C so that k_upd measures drift from C.
-template <int D>
+template <int D, int FC = 4>
 __global__ __launch_bounds__(CAND_TPB) void k_cand(Grid g, const float4 *__restrict__ C, int K,
                                               uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
                                               int32_t *__restrict__ fc_lab, Ctrl *__restrict__ ctrl, int gate,
@@ -1052,7 +1085,7 @@ __global__ __launch_bounds__(CAND_TPB) void k_cand(Grid g, const float4 *__restr
         ctrl->budget = 0.0;
         if (gate) ctrl->rebuilds += 1u;   // lists rebuilt at a relocation resume
     }
-    cand_body<D>(g, C, K, fc_cnt, fc_rec, fc_lab, bpc, 0.0, cl);
+    cand_body<D, FC>(g, C, K, fc_cnt, fc_rec, fc_lab, bpc, 0.0, cl);
 }
 
 // Coarse lists only (one block per coarse cell), for the child blocks of
@@ -1077,36 +1110,18 @@ __global__ __launch_bounds__(CAND_TPB) void k_coarse(Grid g, const float4 *__res
 }
 
 // Candidate records refreshed to the new centres (lists still valid under the
-// drift budget): the children of coarse cell blockIdx.x / BPC handled by this
-// block (the partition of cand_body); CAND_TPB / nch threads per child, every
-// load of a child's count and ids issued in parallel (no per-child loop).
+// drift budget): every fine cell's records, grid-stride over the cells with 16
+// threads per cell, every load of a cell's count and ids issued in parallel.
 template <int D>
 __device__ __forceinline__ void refresh_body(const Grid &g, const float4 *cn, const uint32_t *__restrict__ fc_cnt,
-                                             float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
-                                             int BPC) {
-    const long long I = blockIdx.x / BPC;
-    const int bsub = blockIdx.x % BPC;
-    int ci[MAXD];
-    decode(I, g.GC, D, ci);
-    int nchild = 1;
-    for (int a = 0; a < D; ++a) nchild *= 4;
-    const int cpb = (nchild + BPC - 1) / BPC;
-    const int c0 = bsub * cpb, c1 = min(nchild, (bsub + 1) * cpb);
-    const int per = max(1, CAND_TPB / max(1, c1 - c0));     // threads per child
-    for (int ch = c0 + (int)threadIdx.x / per; ch < c1; ch += CAND_TPB / per) {
-        const int sub = (int)threadIdx.x % per;
-        int f[MAXD];
-        bool inside = true;
-#pragma unroll
-        for (int a = D - 1, t = ch; a >= 0; --a, t >>= 2) {
-            f[a] = ci[a] * 4 + (t & 3);
-            inside &= f[a] < g.G[a];
-        }
-        if (!inside) continue;
-        const long long cell = encode(f, g.G, D);
+                                             float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab) {
+    constexpr int PER = 16, CPB = CAND_TPB / PER;   // threads per cell, cells per block pass
+    const int sub = (int)threadIdx.x % PER;
+    for (long long cell = (long long)blockIdx.x * CPB + (int)threadIdx.x / PER; cell < g.ncells;
+         cell += (long long)gridDim.x * CPB) {
         const uint32_t m = fc_cnt[cell];
         if (m == FULL) continue;
-        for (uint32_t p = sub; p < m; p += per) fc_rec[cell * CAPF + p] = cn[fc_lab[cell * CAPF + p]];
+        for (uint32_t p = sub; p < m; p += PER) fc_rec[cell * CAPF + p] = cn[fc_lab[cell * CAPF + p]];
     }
 }
 
@@ -1203,22 +1218,22 @@ __device__ __forceinline__ void load_x(Raw<T, D> &r, rsrc_t rs, unsigned off_pt)
     }
 }
 #define LOAD_X(dst, off) load_x<T, D>(dst, rx, off)
-// fp32 D = 3 with compressed tiles: the same three b128 loads per item whatever the
-// tile's format (identical vmcnt bookkeeping on every path): raw tiles read
-// x/y/z words at 12 B per point; compressed tiles read lo/hi words at 8 B per
-// point from rA and send the third load out of range (zeros, no traffic).
-__device__ __forceinline__ void load_xa(Raw<float, 3> &r, rsrc_t rA, rsrc_t rx, unsigned off_pt, unsigned bpp, bool zc) {
-    const unsigned boff = off_pt * bpp;
+// compressed item: 4 points' 8-B records, lo words then hi words (AoSoA-4)
+// (templated so that k_lloyd1's other instances, which never call it, compile)
+template <typename R>
+__device__ __forceinline__ void load_z2(R &r, rsrc_t rA, unsigned off_pt) {
+    static_assert(sizeof(r.w) >= 8 * sizeof(unsigned), "compressed items fill 8 words");
+    const unsigned boff = off_pt * 8u;
     const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rA, boff, 0, PCM_XLOAD_CPOL);
     const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rA, boff + 16u, 0, PCM_XLOAD_CPOL);
-    const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rx, zc ? 0xFFFFFFF0u : boff + 32u, 0, PCM_XLOAD_CPOL);
     r.w[0] = v0[0]; r.w[1] = v0[1]; r.w[2] = v0[2]; r.w[3] = v0[3];
     r.w[4] = v1[0]; r.w[5] = v1[1]; r.w[6] = v1[2]; r.w[7] = v1[3];
-    r.w[8] = v2[0]; r.w[9] = v2[1]; r.w[10] = v2[2]; r.w[11] = v2[3];
 }
 // exact fp32 coordinates of a compressed item (k_tile_compress): base + delta bits
-__device__ __forceinline__ void unpack_z(const Raw<float, 3> &r, float (&x)[4][3], const uint4 &zm, unsigned sh1,
+template <typename R, int DD>
+__device__ __forceinline__ void unpack_z(const R &r, float (&x)[4][DD], const uint4 &zm, unsigned sh1,
                                          unsigned sh2, unsigned m0, unsigned m1, unsigned m2) {
+    static_assert(DD == 3 && sizeof(r.w) >= 8 * sizeof(unsigned), "compressed tiles: fp32 D = 3");
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const unsigned lo = r.w[e], hi = r.w[4 + e];
@@ -1311,6 +1326,7 @@ struct LloydArgs {
     Grid g;
     const uint32_t *tl_cnt;         // crowded layouts: per-tile list length for tiles of FULL cells (or FULL), else null
     const float4 *tl_rec;           // [tile][TLCAP] records of the tile lists (k_tile_cand)
+    const float4 *tbox;             // crowded layouts: [tile][2] exact point box (lo, hi), else null
     const int32_t *tl_lab;
 };
 
@@ -1753,9 +1769,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     constexpr int LCAP = CROWD ? TLCAP : CAPF;
     __shared__ float4 crec[LCAP];
     __shared__ int32_t cid[LCAP];
-    // 8 slots (and D = 4): LDS int64 words past them; 12 / 16 slots: global atomics (rare positions)
+    // Lists longer than LS: the LS candidates nearest the tile's centre own the
+    // lane slots (smap: list position -> slot; sid: slot -> centroid), the
+    // rest sum into int64 words per list position -- LDS words (8 slots, D = 4)
+    // or global atomics (12 / 16 slots, rare positions), AccL::gwords when
+    // crowded.  Points mostly pick a candidate near their tile, so the lane
+    // slots take nearly all of them whatever the list's length.
     constexpr bool kOvf = !CROWD && (D >= 4 || LS <= 8);
-    __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
+    __shared__ unsigned long long ovf[kOvf ? CAPF * (D + 1) : 1];
+    __shared__ uint16_t smap[LCAP];
+    __shared__ float skey[LCAP];
+    __shared__ int32_t sid[LS];
     const int tid = threadIdx.x;
     const unsigned t = blockIdx.x;
     // the gate flags, the device tile count and the tile record are loaded
@@ -1815,8 +1839,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         const unsigned o = base0 + (unsigned)rr * 4u * TPB + 4u * tid;
         return (rr < nr && o < end) ? o : 0x0ffffff0u;
     };
+    __shared__ unsigned long long omask[NSUB];
+    __shared__ uint32_t okey[NSUB];
+    __shared__ unsigned long long rmask[16];   // rounds of one tile: <= TILE / (4 TPB) + 1
+    // The rest of the kernel, instantiated per point format: compressed tiles
+    // (fp32 D = 3, 8-B records) issue 2 b128 loads per work item, raw tiles
+    // D * sizeof(T) / 4 -- one constant load count per instance keeps hipcc's
+    // waitcnt bookkeeping exact, and compressed items no longer issue a third,
+    // out-of-range load just to match the raw path's count.
+    auto body = [&](auto ZCc) {
+    constexpr bool ZC = decltype(ZCc)::value;
     auto ldx = [&](Raw<T, D> &dst, unsigned off) {
-        if constexpr (ZOK) load_xa(dst, rA, rx, off, bpp, zc);
+        if constexpr (ZC) load_z2(dst, rA, off);
         else load_x<T, D>(dst, rx, off);
     };
     Raw<T, D> xa, xb, xc;
@@ -1826,33 +1860,68 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     // long tile lists: block-shared int64 words per list position (AccL::gwords, crowded launches only)
     unsigned long long *const govf =
         reinterpret_cast<unsigned long long *>(acc + (AccL<D, LS>::words + 1) / 2 * 2);
-    if (kOvf)
-        for (int e = tid; e < (CAPF - LS) * (D + 1); e += TPB) ovf[e] = 0ull;
     const bool full = (cnt == FULL);
     const int mm = (cnt == FULL) ? A.K : (int)cnt;
+    // block-uniform: the list is longer than the lane slots (not an all-K scan)
+    const bool use_map = !full && mm > LS;
+    if (kOvf && use_map)
+        for (int e = tid; e < mm * (D + 1); e += TPB) ovf[e] = 0ull;
     if (full) {
-        if (tid < LS) cid[tid] = tid;
+        if (tid < LS) sid[tid] = tid;
         // (crowded: positions >= LS of an all-K scan go to global atomics, as the 16-slot variant's)
     } else {
-        if (tl) {   // block-uniform: crowded cells only (r0/l0 hold the cell list)
-            if (tid < LSPEC && tid < mm) {
+        if (tid < LSPEC && tid < mm) {
+            int lab = l0;
+            if (tl) {   // block-uniform: crowded cells only (r0/l0 hold the cell list)
                 crec[tid] = lrec[tid];
-                cid[tid] = llab[tid];
+                lab = llab[tid];
+            } else {
+                crec[tid] = r0;
             }
-        } else if (tid < LSPEC && tid < mm) {
-            crec[tid] = r0;
-            cid[tid] = l0;
+            cid[tid] = lab;
+            if (!use_map) sid[tid] = lab;   // short list: position p owns lane slot p
         }
         for (int j = LSPEC + tid; j < mm; j += TPB) {   // long lists (rare at D <= 3)
             crec[j] = lrec[j];
             cid[j] = llab[j];
         }
-        if (CROWD)
-            for (int j = LS * (D + 1) + tid; j < mm * (D + 1); j += TPB) govf[j] = 0ull;
+        if (CROWD && use_map)
+            for (int j = tid; j < mm * (D + 1); j += TPB) govf[j] = 0ull;
     }
     uint32_t *const myacc = acc + (tid & (AW - 1));
     unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.pstride;
     __syncthreads();
+    if (use_map) {
+        // rank the list by the fp32 squared distance of each candidate to the
+        // tile's centre (ties by position): ranks < LS get the lane slots
+        float ctr[D];
+        if (CROWD && tl && A.tbox) {   // crowded tile: its exact point box
+            const float4 blo = A.tbox[(size_t)t * 2], bhi = A.tbox[(size_t)t * 2 + 1];
+#pragma unroll
+            for (int a = 0; a < D; ++a) ctr[a] = 0.5f * (comp(blo, a) + comp(bhi, a));
+        } else {   // the cell's centre
+            int ci[MAXD];
+            for (int a = D - 1, c = (int)cell; a >= 0; --a) {
+                ci[a] = (int)((unsigned)c % (unsigned)A.g.G[a]);
+                c = (int)((unsigned)c / (unsigned)A.g.G[a]);
+            }
+#pragma unroll
+            for (int a = 0; a < D; ++a) ctr[a] = (float)(A.g.lo[a] + ((double)ci[a] + 0.5) * A.g.w[a]);
+        }
+        for (int j = tid; j < mm; j += TPB) skey[j] = dist_canon<D>(ctr, crec[j]);
+        __syncthreads();
+        for (int j = tid; j < mm; j += TPB) {
+            const float kj = skey[j];
+            int rank = 0;
+            for (int q = 0; q < mm; ++q) {
+                const float kq = skey[q];
+                rank += (kq < kj || (kq == kj && q < j)) ? 1 : 0;
+            }
+            smap[j] = (uint16_t)(rank < LS ? rank : LS + j);
+            if (rank < LS) sid[rank] = cid[j];
+        }
+        __syncthreads();
+    }
     // Sub-cell candidate masks: for every half-cell box (one per axis
     // combination) the list positions its reference does not dominate (the
     // exact test of the candidate lists, at the current centres), then per
@@ -1862,9 +1931,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     // superset of the undominated candidates, scanned in ascending order, gives
     // the exact labels (a dominated candidate is strictly farther for every
     // point of the box, so every tied minimiser is kept).
-    __shared__ unsigned long long omask[NSUB];
-    __shared__ uint32_t okey[NSUB];
-    __shared__ unsigned long long rmask[16];   // rounds of one tile: <= TILE / (4 TPB) + 1
     // only coarse grids (MASK: the 16-slot D <= 3 variant, lists of ~6 at a
     // 12.5M shard: 47.8 -> 43.5 us per launch); at config 3 (lists of ~2.7)
     // and D = 4 (16 sub-cells) the mask phase at the block's start cost more
@@ -1932,7 +1998,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
 
     // loads per work item; after item r+2's are issued, items r+1 and r+2 may
     // stay outstanding while r is computed
-    constexpr int NL = Raw<T, D>::NW / 4 + (Raw<T, D>::NW % 4 ? 1 : 0);
+    constexpr int NL = ZC ? 2 : Raw<T, D>::NW / 4 + (Raw<T, D>::NW % 4 ? 1 : 0);
     constexpr int VM = 2 * NL;
     constexpr int WAIT_PREV = 0x0F70 | (VM & 0xF) | ((VM >> 4) << 14);   // vmcnt(VM) expcnt(7) lgkmcnt(15)
     auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx, int r) {
@@ -1948,12 +2014,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         const unsigned rbase = base0 + (unsigned)r * 4u * TPB;
         const unsigned i0 = rbase + 4u * tid;
         float x[4][D];
-        if constexpr (ZOK) {
-            if (zc) unpack_z(cx, x, zm, zsh1, zsh2, zm0, zm1, zm2);
-            else unpack_x<D>(cx, x);
-        } else {
-            unpack_x<D>(cx, x);
-        }
+        if constexpr (ZC) unpack_z(cx, x, zm, zsh1, zsh2, zm0, zm1, zm2);
+        else unpack_x<D>(cx, x);
         int bj[4];
         if (mm == 1) {
             for (int e = 0; e < 4; ++e) bj[e] = 0;
@@ -1978,39 +2040,42 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         }
         // block-uniform: every point of the round lies inside the tile
         const bool whole = (rbase >= start) && (rbase + 4u * TPB <= end);
-        int sl[4];
+        // slot of each point's winner: its lane slot (< LS), else LS + its list
+        // position (use_map) or, in an all-K scan, LS + (centroid - LS)
+        int sl[4], so[4];
         bool over = false;
         for (int e = 0; e < 4; ++e) {
             const bool v = whole || ((i0 + e >= start) && (i0 + e < end));
-            const bool hi = bj[e] >= LS;
+            const int sm = use_map ? (int)smap[bj[e]] : bj[e];
+            const bool hi = sm >= LS;
             over |= v && hi;
-            sl[e] = (v && !hi) ? bj[e] : LS;
+            sl[e] = (v && !hi) ? sm : LS;
+            so[e] = (v && hi) ? (use_map ? sm - LS : bj[e]) : -1;
         }
         for (int e = 0; e < 4; ++e) {
             uint32_t *ap = myacc + sl[e] * ((D + 1) * AW);
             for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
             atomicAdd(ap + D * AW, 1u);
         }
-        if (over) {   // list positions >= LS (long lists only)
+        if (over) {   // winners without a lane slot (long lists only)
             for (int e = 0; e < 4; ++e) {
-                const bool v = whole || ((i0 + e >= start) && (i0 + e < end));
-                if (!(v && bj[e] >= LS)) continue;
+                const int o = so[e];   // list position (use_map) or centroid (all-K scan)
+                if (o < 0) continue;
                 // one address space per branch (a pointer select would make FLAT
                 // atomics, which count in vmcnt and lgkmcnt and drain the prefetch)
                 if (CROWD && !full) {   // crowded list: block-shared words, folded at the end
-                    unsigned long long *pp = govf + bj[e] * (D + 1);
+                    unsigned long long *pp = govf + o * (D + 1);
                     for (int a = 0; a < D; ++a) atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
                     atomicAdd(pp + D, 1ull);
                 } else if (full || !kOvf) {
-                    unsigned long long *pp = prep + (size_t)(full ? bj[e] : cid[bj[e]]) * (D + 1);
+                    unsigned long long *pp = prep + (size_t)(full ? o : cid[o]) * (D + 1);
                     for (int a = 0; a < D; ++a)
                         atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
                     atomicAdd(pp + D, 1ull);
                 } else {
-                    const int o = (bj[e] - LS) * (D + 1);
-                    for (int a = 0; a < D; ++a)
-                        atomicAdd(&ovf[o + a], (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
-                    atomicAdd(&ovf[o + D], 1ull);
+                    unsigned long long *pp = ovf + o * (D + 1);
+                    for (int a = 0; a < D; ++a) atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                    atomicAdd(pp + D, 1ull);
                 }
             }
         }
@@ -2045,21 +2110,29 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             sacc += __shfl_down(sacc, 1, 16);
             if (pi < npairs && sub == 0 && sacc) {
                 const int slot = pi / (D + 1), qq = pi % (D + 1);
-                atomicAdd(prep + (size_t)cid[slot] * (D + 1) + qq, (unsigned long long)sacc);
+                atomicAdd(prep + (size_t)sid[slot] * (D + 1) + qq, (unsigned long long)sacc);
             }
         }
-        if (CROWD && !full)
-            for (int i = LS * (D + 1) + tid; i < mm * (D + 1); i += TPB) {
+        // the int64 words of the positions without a lane slot (use_map lists)
+        if (CROWD && use_map)
+            for (int i = tid; i < mm * (D + 1); i += TPB) {
                 const unsigned long long w = govf[i];
                 if (w) atomicAdd(prep + (size_t)cid[i / (D + 1)] * (D + 1) + i % (D + 1), w);
             }
-        if (kOvf && !full && mm > LS)
-            for (int i = tid; i < (mm - LS) * (D + 1); i += TPB) {
+        if (kOvf && use_map)
+            for (int i = tid; i < mm * (D + 1); i += TPB) {
                 const unsigned long long w = ovf[i];
-                if (w) atomicAdd(prep + (size_t)cid[LS + i / (D + 1)] * (D + 1) + i % (D + 1), w);
+                if (w) atomicAdd(prep + (size_t)cid[i / (D + 1)] * (D + 1) + i % (D + 1), w);
             }
     }
     DBG_L(3);
+    };
+    if constexpr (ZOK) {
+        if (zc) body(std::true_type{});
+        else body(std::false_type{});
+    } else {
+        body(std::false_type{});
+    }
 }
 
 // Single block of 1024 threads.  Optionally first folds partials[parity] into
@@ -2265,13 +2338,18 @@ constexpr int UPD_TPB = 128;
 constexpr int SHIFT_LANES = 1024;   // oracle/lloyd_ref.py SHIFT_LANES
 constexpr int UPD_LPT = SHIFT_LANES / UPD_TPB;   // tree lanes per thread of the last block
 static_assert(UPD_TPB == 128, "k_upd's last tree steps: one LDS step (h = 64), then wave shuffles");
+// per-block record of k_upd: changed words, empty clusters, max squared drift, max squared shift
+struct UpdPart {
+    unsigned long long neq, nempty, dmax_bits, smax_bits;
+};
 template <int D>
 __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict__ stats_in,
                                                  unsigned long long *__restrict__ partials, int K, QExp qe,
                                                  unsigned long long *__restrict__ held,
                                                  unsigned long long *__restrict__ prev, const float4 *__restrict__ C,
                                                  float4 *__restrict__ Cn, const float4 *__restrict__ cref,
-                                                 double *__restrict__ sh, unsigned long long *__restrict__ hist_changed,
+                                                 double *__restrict__ sh, UpdPart *__restrict__ upart,
+                                                 unsigned long long *__restrict__ hist_changed,
                                                  double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl, double alpha,
                                                  double dl_cap) {
     // the gate flags and the control words this launch reads, in one memory latency
@@ -2287,20 +2365,16 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
     unsigned long long neq = 0ull;
     unsigned ne = 0u;
     double dr = 0.0, ds = 0.0;
+    unsigned long long row[D + 1];
+    float4 cnew = make_float4(0.f, 0.f, 0.f, 0.f);
     if (j < K) {
         const size_t o = (size_t)j * (D + 1);
-        unsigned long long row[D + 1], pv[D + 1];
+        unsigned long long pv[D + 1];
 #pragma unroll
         for (int a = 0; a <= D; ++a) { row[a] = src[o + a]; pv[a] = prev[o + a]; }
         const float4 rj = cref[(size_t)sel * K + j], oj = C[j];
-        unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
 #pragma unroll
-        for (int a = 0; a <= D; ++a) {
-            neq += (row[a] != pv[a]) ? 1ull : 0ull;   // convergence: raw statistics equal the previous ones
-            prev[o + a] = row[a];
-            held[o + a] = row[a];                     // the relocation snapshot, should this iteration halt
-            pnext[o + a] = 0ull;                      // the next accumulation starts from zero
-        }
+        for (int a = 0; a <= D; ++a) neq += (row[a] != pv[a]) ? 1ull : 0ull;   // raw statistics vs the previous ones
         const unsigned long long c = row[D];
         float out[4] = {0.f, 0.f, 0.f, 0.f};
         if (c > 0) {
@@ -2312,16 +2386,29 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
         } else {
             ne = 1u;
         }
-        const float4 v = make_float4(out[0], out[1], out[2], out[3]);
-        Cn[j] = v;
+        cnew = make_float4(out[0], out[1], out[2], out[3]);
 #pragma unroll
         for (int a = 0; a < D; ++a) {
-            const double e1 = (double)comp(v, a) - (double)comp(rj, a);
-            const double e2 = (double)comp(v, a) - (double)comp(oj, a);
+            const double e1 = (double)comp(cnew, a) - (double)comp(rj, a);
+            const double e2 = (double)comp(cnew, a) - (double)comp(oj, a);
             dr += e1 * e1;
             ds += e2 * e2;
         }
         __hip_atomic_store(sh + j, ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // only sh[] is handed to the last block inside this launch: drain it now;
+    // the other stores below are read by later launches (the kernel boundary)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (j < K) {
+        const size_t o = (size_t)j * (D + 1);
+        unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
+#pragma unroll
+        for (int a = 0; a <= D; ++a) {
+            prev[o + a] = row[a];
+            held[o + a] = row[a];   // the relocation snapshot, should this iteration halt
+            pnext[o + a] = 0ull;    // the next accumulation starts from zero
+        }
+        Cn[j] = cnew;
     }
     if (j == 0) {
         held[n] = 0ull;
@@ -2338,43 +2425,57 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
     __shared__ double s_dr[UPD_TPB / 64], s_ds[UPD_TPB / 64];
     __shared__ unsigned s_last;
     if (lane == 0) { s_neq[wv] = neq; s_ne[wv] = ne; s_dr[wv] = dr; s_ds[wv] = ds; }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores of sh
     __syncthreads();
     if (tid == 0) {
         for (int w = 1; w < UPD_TPB / 64; ++w) {
             neq += s_neq[w]; ne += s_ne[w]; dr = fmax(dr, s_dr[w]); ds = fmax(ds, s_ds[w]);
         }
-        if (neq) __hip_atomic_fetch_add(&ctrl->u_neq, neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (ne) __hip_atomic_fetch_add(&ctrl->u_empty, ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // non-negative doubles order like their bit patterns
-        __hip_atomic_fetch_max(&ctrl->u_dmax, (unsigned long long)__double_as_longlong(dr), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_max(&ctrl->u_smax, (unsigned long long)__double_as_longlong(ds), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        // this block's record (sc1 stores, drained before the arrival like sh[])
+        UpdPart *pp = upart + blockIdx.x;
+        __hip_atomic_store(&pp->neq, neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&pp->nempty, (unsigned long long)ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&pp->dmax_bits, (unsigned long long)__double_as_longlong(dr), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&pp->smax_bits, (unsigned long long)__double_as_longlong(ds), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (prior == gridDim.x - 1) ? 1u : 0u;
     }
     __syncthreads();
     if (!s_last) return;
-    // ---- the last block: every other block's stores and atomics have landed
-    const unsigned long long changed = __hip_atomic_load(&ctrl->u_neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned n_empty = __hip_atomic_load(&ctrl->u_empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double dmax = __longlong_as_double(
-        (long long)__hip_atomic_load(&ctrl->u_dmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const double smax = __longlong_as_double(
-        (long long)__hip_atomic_load(&ctrl->u_smax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    __syncthreads();   // every lane has read the totals before lane 0 resets them
-    if (tid == 0) {
-        __hip_atomic_store(&ctrl->u_neq, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctrl->u_empty, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctrl->u_dmax, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctrl->u_smax, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctrl->u_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- the last block: every other block's sh[] and record have landed
+    unsigned long long changed = 0ull, n_empty = 0ull;
+    double dmax = 0.0, smax = 0.0;
+    for (int b = tid; b < (int)gridDim.x; b += UPD_TPB) {
+        const UpdPart *pp = upart + b;
+        changed += __hip_atomic_load(&pp->neq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        n_empty += __hip_atomic_load(&pp->nempty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dmax = fmax(dmax, __longlong_as_double(
+                              (long long)__hip_atomic_load(&pp->dmax_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+        smax = fmax(smax, __longlong_as_double(
+                              (long long)__hip_atomic_load(&pp->smax_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
     }
-    if (n_empty > 0u) {   // empty cluster: the host relocates, then k_global + k_cand resume
+    for (int o = 32; o > 0; o >>= 1) {
+        changed += __shfl_xor(changed, o);
+        n_empty += __shfl_xor(n_empty, o);
+        dmax = fmax(dmax, __shfl_xor(dmax, o));
+        smax = fmax(smax, __shfl_xor(smax, o));
+    }
+    __syncthreads();   // s_* of the arrival phase are reused below
+    if (lane == 0) { s_neq[wv] = changed; s_ne[wv] = (unsigned)n_empty; s_dr[wv] = dmax; s_ds[wv] = smax; }
+    __syncthreads();
+    changed = s_neq[0];
+    n_empty = s_ne[0];
+    dmax = s_dr[0];
+    smax = s_ds[0];
+    for (int w = 1; w < UPD_TPB / 64; ++w) {
+        changed += s_neq[w]; n_empty += s_ne[w]; dmax = fmax(dmax, s_dr[w]); smax = fmax(smax, s_ds[w]);
+    }
+    if (tid == 0) __hip_atomic_store(&ctrl->u_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n_empty > 0ull) {   // empty cluster: the host relocates, then k_global + k_cand resume
         if (tid == 0) {
-            ctrl->n_empty = n_empty;
+            ctrl->n_empty = (unsigned)n_empty;
             ctrl->neq_saved = changed;
             ctrl->lists = 0u;
             ctrl->halt = 1u;
@@ -2440,7 +2541,7 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
 // k_upd: halted iterations leave C untouched (the relocation needs the old
 // centres); queued no-op launches after convergence repeat the same copy and
 // lists (idempotent).
-template <int D>
+template <int D, int FC = 4>
 __global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__restrict__ Cn, float4 *__restrict__ C,
                                                     float4 *__restrict__ cref, int K, const Ctrl *__restrict__ ctrl,
                                                     uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
@@ -2456,8 +2557,8 @@ __global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__rest
         C[j] = c;
         if (mode == 2u) cref[(size_t)sel * K + j] = c;
     }
-    if (mode == 2u) cand_body<D>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
-    else refresh_body<D>(g, Cn, fc_cnt, fc_rec, fc_lab, bpc);
+    if (mode == 2u) cand_body<D, FC>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+    else refresh_body<D>(g, Cn, fc_cnt, fc_rec, fc_lab);
 }
 
 // ------------------------------------------------------------------ relocation

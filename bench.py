@@ -126,6 +126,29 @@ def stereo_bench(H: int = 4000, W: int = 4000, reps: int = 20) -> dict:
         out[name] = {"ms": ms, "GBps": bpp * H * W / (ms * 1e-3) / 1e9, "bytes_per_px": bpp,
                      "frac_hbm": bpp * H * W / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     out["pixels"] = H * W
+    # the product path as disparity_map calls it (pipeline.use_gpu_gathers): host NumPy
+    # arrays in and out -- upload, kernel, download -- beside the NumPy gathers it replaces
+    # (oracle/consistency_ref.py, the reference's processing.py:94-115 / disparity.py:229-250)
+    from oracle import consistency_ref
+    hl, hr, hld, hrd = left.cpu().numpy(), right.cpu().numpy(), ld.cpu().numpy(), rd.cpu().numpy()
+    host = {}
+    for name, gpu_fn, cpu_fn in [
+            ("photoconsistency", lambda: pcm_amd.photoconsistency_map(hl, hr, hld, -144),
+             lambda: consistency_ref.photoconsistency_map(hl, hr, hld, -144)),
+            ("lr_consistency", lambda: pcm_amd.left_right_consistency(hld, hrd, -144),
+             lambda: consistency_ref.left_right_consistency(hld, hrd, -144))]:
+        gpu_fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            g = gpu_fn()
+        gpu_ms = (time.perf_counter() - t0) * 1e3 / 3
+        t0 = time.perf_counter()
+        c = cpu_fn()
+        cpu_ms = (time.perf_counter() - t0) * 1e3
+        assert np.array_equal(g, c)
+        host[name] = {"gpu_host_io_ms": gpu_ms, "numpy_ms": cpu_ms, "speedup": cpu_ms / gpu_ms}
+    out["host_numpy_in_out"] = host
     return out
 
 
