@@ -69,8 +69,8 @@ struct pcm_engine {
     int zlev = 0;
     float4 *tbox = nullptr;          // [tile][2] exact point box
     uint32_t *tl_cnt = nullptr;      // [tile] list length (tiles of FULL cells) or FULL
-    float4 *tl_rec = nullptr;        // [tile][TLCAP]
-    int32_t *tl_lab = nullptr;       // [tile][TLCAP]
+    float4 *tl_rec = nullptr;        // [tile][TLMAX]
+    int32_t *tl_lab = nullptr;       // [tile][TLMAX]
     uint32_t *zcnt = nullptr;        // occupancy sample counts [ncells + 1]
     size_t cap_tbox = 0, cap_tlc = 0, cap_tlr = 0, cap_tll = 0, cap_zcnt = 0;
     uint32_t *perm = nullptr;
@@ -706,8 +706,8 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     if (e->zlev > 0) {   // crowded layout: exact tile boxes and tile-list storage
         HIPCHK(ensure(e->tbox, e->cap_tbox, (size_t)e->ntiles_cap * 2 * sizeof(float4)));
         HIPCHK(ensure(e->tl_cnt, e->cap_tlc, (size_t)e->ntiles_cap * sizeof(uint32_t)));
-        HIPCHK(ensure(e->tl_rec, e->cap_tlr, (size_t)e->ntiles_cap * TLCAP * sizeof(float4)));
-        HIPCHK(ensure(e->tl_lab, e->cap_tll, (size_t)e->ntiles_cap * TLCAP * sizeof(int32_t)));
+        HIPCHK(ensure(e->tl_rec, e->cap_tlr, (size_t)e->ntiles_cap * TLMAX * sizeof(float4)));
+        HIPCHK(ensure(e->tl_lab, e->cap_tll, (size_t)e->ntiles_cap * TLMAX * sizeof(int32_t)));
         rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
             using TT = decltype(T);
             constexpr int D = decltype(DD)::value;
@@ -1030,6 +1030,10 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
                 cl.in_idx = e->cl_idx;
                 k_lists<D, 2><<<(int)n_mid(e), CAND_TPB, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl, e->fc_cnt,
                                                                   e->fc_rec, e->fc_lab, 1, cl);
+            } else if (e->k <= LISTS_STAGE_MAX) {   // centres staged in LDS
+                const int bpc = cand_bpc(e);
+                k_lists<D, 4, true><<<(int)(e->g.ncoarse * bpc), CAND_TPB, (size_t)e->k * sizeof(float4), s>>>(
+                    e->g, e->Cn, e->C, e->cref, e->k, e->ctrl, e->fc_cnt, e->fc_rec, e->fc_lab, bpc, CoarseL{});
             } else {
                 const int bpc = cand_bpc(e);
                 k_lists<D><<<(int)(e->g.ncoarse * bpc), CAND_TPB, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl,

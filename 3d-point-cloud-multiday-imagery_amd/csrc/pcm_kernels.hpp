@@ -30,7 +30,8 @@ constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-
 constexpr int TPB = PCM_TPB;       // assign block size
 constexpr int TILE = 32 * TPB;     // max points per tile: <= 32 per lane, 64 per shared LDS word (see AccL)
 constexpr uint32_t FULL = 0xFFFFFFFFu;
-constexpr int TLCAP = 256;        // tile-list capacity (lists past CAPF are scanned from global memory)
+constexpr int TLCAP = 256;        // tile lists staged whole in k_lloyd1's LDS (slot-map path)
+constexpr int TLMAX = 1024;       // tile-list capacity (longer lists: FULL); lists past TLCAP scan in LDS chunks
 constexpr uint32_t TL_MIN = 16;   // crowded layouts: tiles of cells with longer lists (or FULL) get tile lists
 constexpr int QBITS = 25;
 // Pruning margins (see DESIGN.md "Exactness of pruning").
@@ -574,16 +575,16 @@ __global__ __launch_bounds__(256) void k_tile_cand(const uint4 *__restrict__ til
             total += s_w[w];
         }
         const unsigned pos = off + (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
-        if (keep && pos < (unsigned)TLCAP) {
-            tl_rec[(size_t)t * TLCAP + pos] = C[j];
-            tl_lab[(size_t)t * TLCAP + pos] = j;
+        if (keep && pos < (unsigned)TLMAX) {
+            tl_rec[(size_t)t * TLMAX + pos] = C[j];
+            tl_lab[(size_t)t * TLMAX + pos] = j;
         }
         base += total;
         __syncthreads();   // s_w is rewritten by the next chunk
-        if (base > (unsigned)TLCAP) break;   // block-uniform
+        if (base > (unsigned)TLMAX) break;   // block-uniform
     }
     // FULL: no shorter list than the cell's (the tile scans the cell list, or all K)
-    if (tid == 0) tl_cnt[t] = (base <= (unsigned)TLCAP && base < cc) ? base : FULL;
+    if (tid == 0) tl_cnt[t] = (base <= (unsigned)TLMAX && base < cc) ? base : FULL;
 }
 
 // Tile-list summary: out[0] += tiles of cells past TL_MIN, out[1] += those with a
@@ -1427,8 +1428,8 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned 
         const int32_t *glab = nullptr;      // long tile list: position -> centroid index
         if (tr.w > TL_MIN && A.tl_cnt && A.tl_cnt[t] != FULL) {   // crowded cell: the tile's own list
             const uint32_t tc = A.tl_cnt[t];
-            trec = A.tl_rec + (size_t)t * TLCAP;
-            tlab = A.tl_lab + (size_t)t * TLCAP;
+            trec = A.tl_rec + (size_t)t * TLMAX;
+            tlab = A.tl_lab + (size_t)t * TLMAX;
             tr.w = tc;
             if (tc > (uint32_t)CAPF) { Cs = trec; glab = tlab; }
         }
@@ -1805,9 +1806,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     }
     uint32_t cnt = fc_cnt[cell];
     // crowded cell (list FULL or past TL_MIN): the tile's own list when k_tile_cand built a shorter one
-    // (the all-K and long-list scans read through scalar loads of kernel
-    // arguments: Call / tl_rec, never a selected pointer, which would turn them
-    // into vector loads)
+    // (lists past TLCAP and all-K scans go through LDS in chunks, below)
     const float4 *lrec = fc_rec + (size_t)cell * CAPF;
     const int32_t *llab = fc_lab + (size_t)cell * CAPF;
     bool tl = false;
@@ -1815,8 +1814,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         const uint32_t tc = A.tl_cnt[t];
         if (tc != FULL) {
             cnt = tc;
-            lrec = tl_rec + (size_t)t * TLCAP;
-            llab = A.tl_lab + (size_t)t * TLCAP;
+            lrec = tl_rec + (size_t)t * TLMAX;
+            llab = A.tl_lab + (size_t)t * TLMAX;
             tl = true;
         }
     }
@@ -1862,11 +1861,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         reinterpret_cast<unsigned long long *>(acc + (AccL<D, LS>::words + 1) / 2 * 2);
     const bool full = (cnt == FULL);
     const int mm = (cnt == FULL) ? A.K : (int)cnt;
+    // crowded: an all-K scan or a tile list longer than the LDS list: scanned in
+    // LDS chunks (below), no list staging
+    const bool chunked = CROWD && (full || mm > LCAP);
     // block-uniform: the list is longer than the lane slots (not an all-K scan)
-    const bool use_map = !full && mm > LS;
+    const bool use_map = !full && !chunked && mm > LS;
     if (kOvf && use_map)
         for (int e = tid; e < mm * (D + 1); e += TPB) ovf[e] = 0ull;
-    if (full) {
+    if (full || chunked) {
         if (tid < LS) sid[tid] = tid;
         // (crowded: positions >= LS of an all-K scan go to global atomics, as the 16-slot variant's)
     } else {
@@ -1891,6 +1893,95 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     uint32_t *const myacc = acc + (tid & (AW - 1));
     unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.pstride;
     __syncthreads();
+    if constexpr (CROWD) {
+        if (chunked) {   // block-uniform
+            // Crowded tile with a list longer than TLCAP (up to TLMAX), or FULL (no
+            // list: every centre): the candidates are staged through LDS in chunks
+            // of TLCAP -- the scalar-load scan of a 64-KB centre array missed the
+            // scalar cache every few candidates (~2 ms per 4096-point tile at
+            // K = 4096) -- in ascending centroid index with the strict '<' of scan4
+            // (ties: lowest index).  Winners sum into a direct-mapped LDS table of
+            // int64 words (govf, TLCAP entries tagged with the centroid; a slot
+            // taken by another centroid sends the point to global atomics), folded
+            // into the statistics once at the end.
+            constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+            __shared__ uint32_t htag[TLCAP];
+            for (int h = tid; h < TLCAP; h += TPB) htag[h] = EMPTY;
+            for (int e = tid; e < TLCAP * (D + 1); e += TPB) govf[e] = 0ull;
+            const rsrc_t rxf = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
+            for (int r = 0; r < nr; ++r) {
+                const unsigned rbase = base0 + (unsigned)r * 4u * TPB;
+                const unsigned i0 = rbase + 4u * tid;
+                const unsigned off = (i0 < end) ? i0 : 0x0ffffff0u;
+                float x[4][D];
+                if constexpr (ZOK) {
+                    Raw<float, 3> raw;
+                    if (zc) {
+                        load_z2(raw, rA, off);
+                        unpack_z(raw, x, zm, zsh1, zsh2, zm0, zm1, zm2);
+                    } else {
+                        load_x<float, 3>(raw, rxf, off);
+                        unpack_x<3>(raw, x);
+                    }
+                } else {
+                    Raw<T, D> raw;
+                    load_x<T, D>(raw, rxf, off);
+                    unpack_x<D>(raw, x);
+                }
+                float bd[4];
+                int bj[4];
+                for (int c0 = 0; c0 < mm; c0 += TLCAP) {
+                    const int mc = min(TLCAP, mm - c0);
+                    __syncthreads();   // the previous chunk has been scanned
+                    if (full) {
+                        for (int j = tid; j < mc; j += TPB) { crec[j] = Call[c0 + j]; cid[j] = c0 + j; }
+                    } else {
+                        for (int j = tid; j < mc; j += TPB) { crec[j] = lrec[c0 + j]; cid[j] = llab[c0 + j]; }
+                    }
+                    __syncthreads();
+                    int j = 0;
+                    if (c0 == 0) {
+                        const float4 c = crec[0];
+                        const int cj = cid[0];
+                        for (int e = 0; e < 4; ++e) { bd[e] = dist_canon<D>(x[e], c); bj[e] = cj; }
+                        j = 1;
+                    }
+                    for (; j < mc; ++j) {
+                        const float4 c = crec[j];
+                        const int cj = cid[j];
+                        for (int e = 0; e < 4; ++e) {
+                            const float dd = dist_canon<D>(x[e], c);
+                            const bool lt = dd < bd[e];
+                            bd[e] = lt ? dd : bd[e];
+                            bj[e] = lt ? cj : bj[e];
+                        }
+                    }
+                }
+                for (int e = 0; e < 4; ++e) {
+                    if (!((i0 + e >= start) && (i0 + e < end))) continue;
+                    const uint32_t h = (uint32_t)bj[e] & (uint32_t)(TLCAP - 1);
+                    const uint32_t old = atomicCAS(&htag[h], EMPTY, (uint32_t)bj[e]);
+                    if (old == EMPTY || old == (uint32_t)bj[e]) {
+                        unsigned long long *pp = govf + h * (D + 1);
+                        for (int a = 0; a < D; ++a) atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                        atomicAdd(pp + D, 1ull);
+                    } else {
+                        unsigned long long *pp = prep + (size_t)bj[e] * (D + 1);
+                        for (int a = 0; a < D; ++a)
+                            atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
+                        atomicAdd(pp + D, 1ull);
+                    }
+                }
+            }
+            __syncthreads();
+            for (int i = tid; i < TLCAP * (D + 1); i += TPB) {
+                const uint32_t c = htag[i / (D + 1)];
+                const unsigned long long w = govf[i];
+                if (c != EMPTY && w) atomicAdd(prep + (size_t)c * (D + 1) + i % (D + 1), w);
+            }
+            return;
+        }
+    }
     if (use_map) {
         // rank the list by the fp32 squared distance of each candidate to the
         // tile's centre (ties by position): ranks < LS get the lane slots
@@ -2541,7 +2632,8 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
 // k_upd: halted iterations leave C untouched (the relocation needs the old
 // centres); queued no-op launches after convergence repeat the same copy and
 // lists (idempotent).
-template <int D, int FC = 4>
+constexpr int LISTS_STAGE_MAX = 2048;   // k_lists stages the centres in LDS up to this K (32 KB)
+template <int D, int FC = 4, bool STAGE = false>
 __global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__restrict__ Cn, float4 *__restrict__ C,
                                                     float4 *__restrict__ cref, int K, const Ctrl *__restrict__ ctrl,
                                                     uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
@@ -2557,8 +2649,21 @@ __global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__rest
         C[j] = c;
         if (mode == 2u) cref[(size_t)sel * K + j] = c;
     }
-    if (mode == 2u) cand_body<D, FC>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
-    else refresh_body<D>(g, Cn, fc_cnt, fc_rec, fc_lab);
+    if (mode != 2u) {
+        refresh_body<D>(g, Cn, fc_cnt, fc_rec, fc_lab);
+        return;
+    }
+    if constexpr (STAGE) {
+        // all K new centres staged in LDS by one coalesced pass: the list phases'
+        // reads of them (references, tests, compaction) become LDS reads instead
+        // of dependent global round trips
+        extern __shared__ __attribute__((aligned(16))) float4 cstage[];
+        for (int j = threadIdx.x; j < K; j += CAND_TPB) cstage[j] = Cn[j];
+        __syncthreads();
+        cand_body<D, FC>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+    } else {
+        cand_body<D, FC>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+    }
 }
 
 // ------------------------------------------------------------------ relocation
