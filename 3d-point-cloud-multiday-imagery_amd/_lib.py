@@ -33,7 +33,7 @@ EXPORTS = [
     "pcm_dense_status", "pcm_dense_outputs", "pcm_dense_kmeanspp_workspace", "pcm_dense_kmeanspp",
     "pcm_photoconsistency", "pcm_lr_consistency",
     "pcm_layout_shard", "pcm_shard_hist", "pcm_shard_partition_workspace", "pcm_shard_partition",
-    "pcm_shard_scatter_labels", "pcm_assign_kernel_name", "pcm_layout_stream_bytes",
+    "pcm_shard_scatter_labels", "pcm_assign_kernel_name", "pcm_layout_stream_bytes", "pcm_engine_reserve",
 ]
 ABI_VERSION = 4
 
@@ -81,6 +81,7 @@ def _declare(lib):
         "pcm_engine_destroy": ([P], I),
         "pcm_layout_bbox": ([P, P, I64, P, P, P, P], I),
         "pcm_layout_build": ([P, P, P, I64, P], I),
+        "pcm_engine_reserve": ([P, I64, P], I),
         "pcm_fit_begin": ([P, P, D, I, P], I),
         "pcm_iter_local": ([P, P], I),
         "pcm_iter_global": ([P, P], I),

@@ -52,7 +52,14 @@ class Engine:
                                               self.max_iter_cap, ctypes.byref(h)), "pcm_engine_create")
         self.h = h
         self.n = 0
-        self.stats = None
+        # statistics live in a torch tensor so torch.distributed can all-reduce them;
+        # allocated (and torch's fill kernel loaded) here, at engine creation, not in
+        # the first layout (pcm_fit_begin zeroes them for every fit)
+        cnt = ctypes.c_int64()
+        p = ctypes.c_void_p()
+        _lib.check(self.lib.pcm_stats_ptr(self.h, ctypes.byref(p), ctypes.byref(cnt)), "pcm_stats_ptr")
+        self.stats = torch.zeros(cnt.value, dtype=torch.int64, device=self.device)
+        _lib.check(self.lib.pcm_bind_stats(self.h, _ptr(self.stats)), "pcm_bind_stats")
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
@@ -64,6 +71,12 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+    def reserve(self, n: int):
+        """Grow the point-sized device buffers for layouts of up to ``n`` points
+        now (``pcm_engine_reserve``): a fresh process's first large allocations
+        map and clear new VRAM, which would otherwise land in the first layout."""
+        _lib.check(self.lib.pcm_engine_reserve(self.h, int(n), _stream()), "pcm_engine_reserve")
 
     # ------------------------------------------------------------ layout
     def bbox(self, X: torch.Tensor):
@@ -83,12 +96,6 @@ class Engine:
         _lib.check(self.lib.pcm_layout_build(self.h, _ptr(X) if X.numel() else None,
                                              qa.ctypes.data_as(ctypes.c_void_p), int(gidx0), _stream()),
                    "pcm_layout_build")
-        cnt = ctypes.c_int64()
-        p = ctypes.c_void_p()
-        self.lib.pcm_stats_ptr(self.h, ctypes.byref(p), ctypes.byref(cnt))
-        # statistics live in a torch tensor so torch.distributed can all-reduce them
-        self.stats = torch.zeros(cnt.value, dtype=torch.int64, device=self.device)
-        _lib.check(self.lib.pcm_bind_stats(self.h, _ptr(self.stats)), "pcm_bind_stats")
 
     def set_shard(self, rows: torch.Tensor, n_global: int):
         """This engine's cloud is a spatial shard (``pcm_layout_shard``): global

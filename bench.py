@@ -410,7 +410,12 @@ def main():
     max_iter = 2 * total_iters + 16      # timed steps + the eager event pass of as many
     group = None
     eng = Engine(D, K, pdt, max_iter=max_iter)
+    # engine setup: the point-sized device buffers grown (and the fresh VRAM mapped)
+    # before the timed layout -- a spatial slab holds ~N/world points, 1/8 headroom
+    t0 = time.perf_counter()
+    eng.reserve(int(X.shape[0] * (1.125 if world > 1 and args.shard == "slab" else 1.0)))
     torch.cuda.synchronize()
+    reserve_ms = (time.perf_counter() - t0) * 1e3
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -587,6 +592,7 @@ def main():
                                       "tile_lists": tm.get("candidates_ms", 0.0)},
             "candidates": cand,
             "layout_ms": layout_ms,
+            "reserve_ms": reserve_ms,   # engine setup (Engine.reserve), before the timed layout
         }
         if getattr(args, "graph_error", None):
             out["graph_error"] = args.graph_error

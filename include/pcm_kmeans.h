@@ -102,6 +102,13 @@ int pcm_layout_bbox(pcm_engine *e, const void *X, int64_t n, void *stream,
  * this call returns. */
 int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gidx0, void *stream);
 
+/* Optional, at engine setup: grow (and zero) the point-sized device buffers a
+ * layout of up to `n` points needs, so that the first pcm_layout_build of a
+ * process allocates nothing large (a fresh process's first allocations map
+ * and clear new VRAM).  Buffers only grow; invalidates the current layout.
+ * No reference counterpart (the reference allocates per call). */
+int pcm_engine_reserve(pcm_engine *e, int64_t n, void *stream);
+
 /* Layout, optional step between pcm_layout_bbox and pcm_layout_build: the
  * engine's cloud is a SPATIAL shard of a fit over `n_global` points on all
  * ranks (pcm_shard_* below).  `rows` (device uint32[n], copied) is each local

@@ -309,3 +309,23 @@ def test_lane_slot_variants(pcm, slots, monkeypatch):
     ref = R.lloyd_fit(X, C0, max_iter=6, fast=True)
     res = gpu_fit(pcm, X, C0, 6)
     assert_same(res, ref, f"long lists, {slots} slots")
+
+
+def test_engine_reserve(pcm):
+    """pcm_engine_reserve (engine setup) grows the point-sized buffers: fits on a
+    reserved engine -- smaller, then larger clouds than reserved -- stay exact."""
+    from pcm_amd.engine import Engine
+    eng = Engine(3, 256, torch.float32, max_iter=8)
+    eng.reserve(150_000)
+    for n, seed in ((120_000, 21), (150_000, 22), (260_000, 23)):
+        X = R.splitmix_uniform(n, 3, seed)
+        C0 = X[R.init_indices(n, 256)]
+        ref = R.lloyd_fit(X, C0, max_iter=8, fast=True)
+        res = pcm.lloyd_fit(torch.from_numpy(X).cuda(), torch.from_numpy(C0).cuda(), max_iter=8, tol=0.0,
+                            engine=eng)
+        assert_same(res, ref, f"reserved engine n={n}")
+    eng.reserve(400_000)            # invalidates the layout: iterating needs a new one
+    from pcm_amd._lib import PcmError
+    with pytest.raises(PcmError):
+        eng.iterate(1)
+    eng.close()
