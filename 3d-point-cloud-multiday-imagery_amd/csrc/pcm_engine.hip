@@ -600,7 +600,7 @@ int pcm_engine_reserve(pcm_engine *e, int64_t n, void *stream) {
         {(void **)&e->perm, &e->cap_perm, (size_t)n * sizeof(uint32_t)},
         {(void **)&e->ws, &e->cap_ws, ws_need},
         {(void **)&e->dmap, &e->cap_dmap, (size_t)2 * n * sizeof(uint32_t)},
-        {(void **)&e->xz, &e->cap_xz, (e->dtype == PCM_F32 && e->d == 3) ? (size_t)npad * 8 : 0},
+        {(void **)&e->xz, &e->cap_xz, (e->dtype == PCM_F32 && e->d == 3) ? (size_t)align_up(npad) * 8 : 0},
     };
     free_layout(e);   // a grown buffer no longer holds the old layout
     for (const Buf &b : bufs) {
@@ -742,7 +742,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     e->use_xz = xz_on && e->dtype == PCM_F32 && e->d == 3;
     HIPCHK(hipMemsetAsync(e->zpts, 0, 32 * 16 * sizeof(unsigned long long), s));
     if (e->use_xz) {
-        HIPCHK(ensure(e->xz, e->cap_xz, (size_t)e->npad * 8));
+        HIPCHK(ensure(e->xz, e->cap_xz, (size_t)align_up(e->npad) * 8));   // whole 256-point blocks (zword)
         HIPCHK(ensure(e->tmeta, e->cap_tmeta, (size_t)e->ntiles_cap * sizeof(uint4)));
         k_tile_compress<<<(int)e->ntiles_cap, 256, 0, s>>>((const float *)e->xs, e->tiles, e->ntiles_dev, e->tmeta,
                                                            e->xz, e->zpts);
@@ -1062,9 +1062,39 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
             double wmin = 0.0;
             for (int a = 0; a < D; ++a)
                 if (e->g.ext[a] > 0 && (wmin == 0.0 || e->g.w[a] < wmin)) wmin = e->g.w[a];
-            k_upd<D><<<blocks_for(e->k, UPD_TPB), UPD_TPB, 0, s>>>(
-                from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->Cn, e->cref,
-                e->shbuf, e->upart, e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin);
+            // D <= 3, K <= 1024: update and lists in one launch (k_updlists)
+            static const bool fused_on = [] { const char *v = std::getenv("PCM_FUSED_UPD"); return v && std::atoi(v) != 0; }();
+            if (fused_on && D <= 3 && !split_coarse(e) && e->k <= 2 * CAND_TPB) {
+                const int bpc = cand_bpc(e);
+                auto fused = [&](auto RR) {
+                    k_updlists<D, decltype(RR)::value><<<(int)(e->g.ncoarse * bpc), CAND_TPB,
+                                                         (size_t)e->k * sizeof(float4), s>>>(
+                        from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->cref,
+                        e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin, e->g,
+                        e->fc_cnt, e->fc_rec, e->fc_lab, bpc);
+                };
+                if (e->k <= CAND_TPB) fused(std::integral_constant<int, 1>{});
+                else fused(std::integral_constant<int, 2>{});
+                LAUNCHCHK();
+                return 0;
+            }
+            // one block (the shift tree in LDS, no hand-off between blocks) up to UPD1_MAX centres
+            auto upd1 = [&](auto RR) {
+                k_upd1<D, decltype(RR)::value><<<1, SHIFT_LANES, 0, s>>>(
+                    from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->Cn,
+                    e->cref, e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin);
+            };
+            if (e->k <= SHIFT_LANES)
+                upd1(std::integral_constant<int, 1>{});
+            else if (e->k <= 2 * SHIFT_LANES)
+                upd1(std::integral_constant<int, 2>{});
+            else if (e->k <= UPD1_MAX)
+                upd1(std::integral_constant<int, 4>{});
+            else
+                k_upd<D><<<blocks_for(e->k, UPD_TPB), UPD_TPB, 0, s>>>(
+                    from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->Cn,
+                    e->cref, e->shbuf, e->upart, e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha,
+                    e->drift_kappa * wmin);
             LAUNCHCHK();
             if (split_coarse(e)) {
                 if (int rc = ensure_coarse(e)) return rc;

@@ -352,13 +352,36 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
 // patterns of same-signed floats are ordered by magnitude).  When every axis is
 // single-signed over the tile and the three delta widths sum to <= 64 bits, the
 // tile's points are stored as 8-byte records d0 | d1 << w0 | d2 << (w0 + w1) in
-// `xz` (AoSoA-4: [lo0 lo1 lo2 lo3][hi0 hi1 hi2 hi3] per group of 4 points, at
-// byte 8 * position); k_lloyd1 then streams 8 instead of 12 bytes per point and
+// `xz` (lo and hi words, zword() below); k_lloyd1 then streams 8 instead of 12 bytes per point and
 // rebuilds the EXACT fp32 values (lossless: labels and sums are unchanged).
 // tmeta[t] = {min0, min1, min2, 1 << 31 | w0 | w1 << 8 | w2 << 16}, or .w = 0
 // (raw tile: 12-B AoSoA-4 `xs`).  Uniform [0,1)^3 cloud with 32^3 cells: cells
 // with an axis index >= 1 need <= 23 + 21 + 20 bits; ~91 % of the points.
 __device__ __forceinline__ unsigned zwidth(unsigned span) { return span ? 32u - (unsigned)__clz(span) : 0u; }
+
+// Word offset in `xz` of the lo word of point i (its hi word: + ZHI).  PCM_ZWAVE
+// (default): blocks of 256 points, 1 KB of lo words then 1 KB of hi words, each
+// group of 4 points' words 16 B at (i % 256) / 4 -- a wave's 64 lanes x 4 points
+// load 2 x 1 KB of consecutive bytes (two b128 per lane, each instruction one
+// contiguous run).  PCM_ZWAVE=0: [lo0..lo3][hi0..hi3] per group (32 B per lane:
+// each b128 instruction reads every other 16 B).
+#ifndef PCM_ZWAVE
+#define PCM_ZWAVE 1
+#endif
+// Record fields: x = bits [0, w0), y = [w0, w0 + w1), z = the top w2 bits
+// (PCM_ZTOP, default: x by a mask, y by one funnel shift of the two words, z by
+// one shift of the high word -- 7 VALU per point) or z = [w0 + w1, w0 + w1 + w2)
+// (PCM_ZTOP=0: two 64-bit shifts, ~11 VALU per point).
+#ifndef PCM_ZTOP
+#define PCM_ZTOP 1
+#endif
+#if PCM_ZWAVE
+constexpr unsigned ZHI = 256;
+__host__ __device__ __forceinline__ size_t zword(size_t i) { return (i >> 8) * 512u + (i & 255u); }
+#else
+constexpr unsigned ZHI = 4;
+__host__ __device__ __forceinline__ size_t zword(size_t i) { return (i >> 2) * 8u + (i & 3u); }
+#endif
 
 __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__ xs, const uint4 *__restrict__ tiles,
                                                        const uint32_t *__restrict__ ntiles, uint4 *__restrict__ tmeta,
@@ -417,6 +440,10 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
             ok = ok && (so == sa) && w[a] <= 31u;
             total += w[a];
         }
+        // the z field sits at the top of the 64-bit record (decoded by one shift of
+        // the high word): at least 1 bit wide, so the shift stays below 32
+        // (w0 + w1 <= 62: the extra bit always fits)
+        if (PCM_ZTOP && w[2] == 0u) { w[2] = 1u; ++total; }
         ok = ok && total <= 64u;
         meta = make_uint4(lo[0], lo[1], lo[2], ok ? (0x80000000u | w[0] | (w[1] << 8) | (w[2] << 16)) : 0u);
         tmeta[t] = meta;
@@ -425,7 +452,7 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
     __syncthreads();
     const uint4 m = meta;
     if (!(m.w >> 31)) return;
-    const unsigned w0 = m.w & 0xffu, w1 = (m.w >> 8) & 0xffu;
+    const unsigned w0 = m.w & 0xffu, w1 = (m.w >> 8) & 0xffu, w2 = (m.w >> 16) & 0xffu;
 #pragma unroll
     for (int u = 0; u < PPT; ++u) {
         const unsigned i = start + tid + 256u * u;
@@ -433,10 +460,10 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
         const unsigned long long d0 = bits[u][0] - m.x;
         const unsigned long long d1 = bits[u][1] - m.y;
         const unsigned long long d2 = bits[u][2] - m.z;
-        const unsigned long long v = d0 | (d1 << w0) | (d2 << (w0 + w1));
-        const size_t g = (size_t)(i >> 2) * 8u + (i & 3u);
+        const unsigned long long v = d0 | (d1 << w0) | (d2 << (PCM_ZTOP ? 64u - w2 : w0 + w1));
+        const size_t g = zword(i);
         xz[g] = (unsigned)v;
-        xz[g + 4] = (unsigned)(v >> 32);
+        xz[g + ZHI] = (unsigned)(v >> 32);
     }
 }
 
@@ -1224,13 +1251,16 @@ __device__ __forceinline__ void load_x(Raw<T, D> &r, rsrc_t rs, unsigned off_pt)
 template <typename R>
 __device__ __forceinline__ void load_z2(R &r, rsrc_t rA, unsigned off_pt) {
     static_assert(sizeof(r.w) >= 8 * sizeof(unsigned), "compressed items fill 8 words");
-    const unsigned boff = off_pt * 8u;
+    // off_pt is a multiple of 4 (or the out-of-range 0x0ffffff0: offsets past any
+    // buffer, zeros without memory traffic)
+    const unsigned boff = off_pt >= 0x0ffffff0u ? 0xfffff000u : (unsigned)zword(off_pt) * 4u;
     const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rA, boff, 0, PCM_XLOAD_CPOL);
-    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rA, boff + 16u, 0, PCM_XLOAD_CPOL);
+    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rA, boff + 4u * ZHI, 0, PCM_XLOAD_CPOL);
     r.w[0] = v0[0]; r.w[1] = v0[1]; r.w[2] = v0[2]; r.w[3] = v0[3];
     r.w[4] = v1[0]; r.w[5] = v1[1]; r.w[6] = v1[2]; r.w[7] = v1[3];
 }
 // exact fp32 coordinates of a compressed item (k_tile_compress): base + delta bits
+// (sh1 = w0; sh2 = 32 - w2 with PCM_ZTOP, else w0 + w1)
 template <typename R, int DD>
 __device__ __forceinline__ void unpack_z(const R &r, float (&x)[4][DD], const uint4 &zm, unsigned sh1,
                                          unsigned sh2, unsigned m0, unsigned m1, unsigned m2) {
@@ -1238,10 +1268,15 @@ __device__ __forceinline__ void unpack_z(const R &r, float (&x)[4][DD], const ui
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const unsigned lo = r.w[e], hi = r.w[4 + e];
-        const unsigned long long v = ((unsigned long long)hi << 32) | lo;
         x[e][0] = __uint_as_float(zm.x + (lo & m0));
+#if PCM_ZTOP
+        x[e][1] = __uint_as_float(zm.y + (__builtin_amdgcn_alignbit(hi, lo, sh1) & m1));
+        x[e][2] = __uint_as_float(zm.z + (hi >> sh2));
+#else
+        const unsigned long long v = ((unsigned long long)hi << 32) | lo;
         x[e][1] = __uint_as_float(zm.y + ((unsigned)(v >> sh1) & m1));
         x[e][2] = __uint_as_float(zm.z + ((unsigned)(v >> sh2) & m2));
+#endif
     }
 }
 // AoSoA-4 (xs_index): word a*4 + e holds coordinate a of the lane's point e
@@ -1753,8 +1788,13 @@ constexpr int MASK_MIN = PCM_MASK_MIN;   // sub-cell masks for lists of at least
 // only 212.5 -> 211.3 us: the kernel is memory-bound, residency was not the
 // limit); the masked 16-slot variant spills at 6 (12.5M shard
 // 42.0 -> 45.5 us) and D = 4 gains nothing, so they keep 4.
+// Work items of a compressed tile in flight while one is computed (raw tiles: 2).
+#ifndef PCM_ZPF
+#define PCM_ZPF 2
+#endif
+constexpr int ZPF = PCM_ZPF;
 template <typename T, int D, int LS, bool MASK>
-constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? 6 : PCM_WPE; }
+constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? (ZPF > 2 ? 5 : 6) : PCM_WPE; }
 
 // CROWD: the crowded-layout instance (tile lists, long lists, AccL::gwords of
 // dynamic LDS); the other instances compile without that code.
@@ -1829,10 +1869,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     // compressed tile (k_tile_compress): 8-B records from xz, decoded exactly
     const bool zc = ZOK && (zm.w >> 31);
     const unsigned zw0 = zm.w & 0xffu, zw1 = (zm.w >> 8) & 0xffu, zw2 = (zm.w >> 16) & 0xffu;
-    const unsigned zsh1 = zw0, zsh2 = zw0 + zw1;
+    const unsigned zsh1 = zw0, zsh2 = PCM_ZTOP ? 32u - zw2 : zw0 + zw1;
     const unsigned zm0 = (1u << zw0) - 1u, zm1 = (1u << zw1) - 1u, zm2 = (1u << zw2) - 1u;
     const unsigned bpp = zc ? 8u : (unsigned)(D * sizeof(T));
-    const rsrc_t rA = make_rsrc(zc ? (const void *)A.xz : A.xs, (unsigned long long)A.npad * bpp);
+    const rsrc_t rA = make_rsrc(zc ? (const void *)A.xz : A.xs, (unsigned long long)(zc ? (A.npad + 255) / 256 * 256 : A.npad) * bpp);
     // lanes past the tile's end get the out-of-range offset: zeros, no memory traffic
     auto item_off = [&](int rr) -> unsigned {
         const unsigned o = base0 + (unsigned)rr * 4u * TPB + 4u * tid;
@@ -1852,9 +1892,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         if constexpr (ZC) load_z2(dst, rA, off);
         else load_x<T, D>(dst, rx, off);
     };
-    Raw<T, D> xa, xb, xc;
-    ldx(xa, item_off(0));
-    ldx(xb, item_off(1));
+    // work items r+1 .. r+PF in flight while item r is computed: a ring of PF+1
+    // register sets (compile-time indices after unrolling)
+    constexpr int PF = ZC ? ZPF : 2;
+    Raw<T, D> xr[PF + 1];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) ldx(xr[k], item_off(k));
     for (int e = tid; e < AccL<D, LS>::words; e += TPB) acc[e] = 0u;
     // long tile lists: block-shared int64 words per list position (AccL::gwords, crowded launches only)
     unsigned long long *const govf =
@@ -1866,6 +1909,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     const bool chunked = CROWD && (full || mm > LCAP);
     // block-uniform: the list is longer than the lane slots (not an all-K scan)
     const bool use_map = !full && !chunked && mm > LS;
+    // block-uniform: a winner can lack a lane slot only in an all-K scan or a
+    // list longer than the slots (the per-round test below is skipped otherwise)
+    const bool can_over = full || mm > LS;
     if (kOvf && use_map)
         for (int e = tid; e < mm * (D + 1); e += TPB) ovf[e] = 0ull;
     if (full || chunked) {
@@ -2087,13 +2133,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     }
     DBG_L(1);
 
-    // loads per work item; after item r+2's are issued, items r+1 and r+2 may
+    // loads per work item; after item r+PF's are issued, items r+1 .. r+PF may
     // stay outstanding while r is computed
     constexpr int NL = ZC ? 2 : Raw<T, D>::NW / 4 + (Raw<T, D>::NW % 4 ? 1 : 0);
-    constexpr int VM = 2 * NL;
+    constexpr int VM = PF * NL;
     constexpr int WAIT_PREV = 0x0F70 | (VM & 0xF) | ((VM >> 4) << 14);   // vmcnt(VM) expcnt(7) lgkmcnt(15)
     auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx, int r) {
-        ldx(nx, item_off(r + 2));
+        ldx(nx, item_off(r + PF));
         if (r >= nr) {
             // padding step (nr not a multiple of 3): no compute, but the same
             // wait as a computing step, so that every path reaches the loop
@@ -2148,7 +2194,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
             atomicAdd(ap + D * AW, 1u);
         }
-        if (over) {   // winners without a lane slot (long lists only)
+        if (can_over && over) {   // winners without a lane slot (long lists only)
             for (int e = 0; e < 4; ++e) {
                 const int o = so[e];   // list position (use_map) or centroid (all-K scan)
                 if (o < 0) continue;
@@ -2171,12 +2217,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             }
         }
     };
-    // three rotating register sets: work items r+1 and r+2 in flight while r is
-    // computed; a tile holds at most TILE / (4 TPB) = 8 rounds
-    for (int r = 0; r < nr; r += 3) {
-        step(xa, xc, r);
-        step(xb, xa, r + 1);
-        step(xc, xb, r + 2);
+    // PF+1 rotating register sets; a tile holds at most TILE / (4 TPB) = 8 rounds
+    for (int r = 0; r < nr; r += PF + 1) {
+#pragma unroll
+        for (int k = 0; k <= PF; ++k) step(xr[k], xr[(k + PF) % (PF + 1)], r + k);
     }
     DBG_L(2);
     // fold the slot words into the int64 statistics: 16 threads per (slot, a) row
@@ -2433,6 +2477,79 @@ static_assert(UPD_TPB == 128, "k_upd's last tree steps: one LDS step (h = 64), t
 struct UpdPart {
     unsigned long long neq, nempty, dmax_bits, smax_bits;
 };
+// centroid j's loads: its statistics row, the previous row, the lists'
+// reference position and the current centre
+template <int D>
+__device__ __forceinline__ void upd_load(int j, int K, const unsigned long long *src, const unsigned long long *prev,
+                                         const float4 *cref, unsigned sel, const float4 *C,
+                                         unsigned long long (&row)[D + 1], unsigned long long (&pv)[D + 1],
+                                         float4 &rj, float4 &oj) {
+    const size_t o = (size_t)j * (D + 1);
+#pragma unroll
+    for (int a = 0; a <= D; ++a) { row[a] = src[o + a]; pv[a] = prev[o + a]; }
+    rj = cref[(size_t)sel * K + j];
+    oj = C[j];
+}
+// its new centre (_average_centers: one fp64 division, one rounding to fp32),
+// changed statistic words, emptiness, squared drift and squared shift
+template <int D>
+__device__ __forceinline__ void upd_row(const unsigned long long (&row)[D + 1], const unsigned long long (&pv)[D + 1],
+                                        const float4 &rj, const float4 &oj, const QExp &qe, float4 &cnew,
+                                        unsigned long long &neq, unsigned &ne, double &dr, double &ds) {
+#pragma unroll
+    for (int a = 0; a <= D; ++a) neq += (row[a] != pv[a]) ? 1ull : 0ull;   // raw statistics vs the previous ones
+    const unsigned long long c = row[D];
+    float out[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c > 0) {
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const double m = ((double)(long long)row[a] * __builtin_ldexp(1.0, -qe.q[a])) / (double)c;
+            out[a] = (float)m;
+        }
+    } else {
+        ne += 1u;
+    }
+    cnew = make_float4(out[0], out[1], out[2], out[3]);
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        const double e1 = (double)comp(cnew, a) - (double)comp(rj, a);
+        const double e2 = (double)comp(cnew, a) - (double)comp(oj, a);
+        dr += e1 * e1;
+        ds += e2 * e2;
+    }
+}
+// one lane: history, convergence flags and the list work of the next launch
+// (it, max_iter, budget, tol: the control words as this launch found them)
+__device__ __forceinline__ void upd_publish(Ctrl *ctrl, unsigned long long changed, double shift, double dmax,
+                                            double smax, unsigned sel, double alpha, double dl_cap,
+                                            unsigned long long *hist_changed, double *hist_shift, uint32_t it,
+                                            uint32_t max_iter, double budget, double tol) {
+    if (it < max_iter) {
+        hist_changed[it] = changed;
+        hist_shift[it] = shift;
+    }
+    ctrl->last_changed = changed;
+    ctrl->last_shift = shift;
+    ctrl->resume = 0u;
+    const double slack = 1.0 + 9.094947017729282e-13;   // 1 + 2^-40: fp64 rounding of the drift norms
+    const bool rebuild = !(sqrt(dmax) * slack <= budget);
+    double dl_new = alpha * sqrt(smax) * slack;
+    if (!(dl_new <= dl_cap)) dl_new = 0.0;
+    if (rebuild) {
+        ctrl->ref_sel = sel ^ 1u;
+        ctrl->budget = dl_new;
+        ctrl->rebuilds += 1u;
+    }
+    ctrl->lists = rebuild ? 2u : 1u;
+    ctrl->lists_dl = rebuild ? dl_new : budget;
+    uint32_t done = 0;
+    if (changed == 0ull) done = 1u;
+    else if (shift <= tol) done = 2u;
+    if (!done && it + 1 >= max_iter) done = 3u;
+    ctrl->done = done;
+    ctrl->iter = it + 1;
+}
+
 template <int D>
 __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict__ stats_in,
                                                  unsigned long long *__restrict__ partials, int K, QExp qe,
@@ -2456,35 +2573,12 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
     unsigned long long neq = 0ull;
     unsigned ne = 0u;
     double dr = 0.0, ds = 0.0;
-    unsigned long long row[D + 1];
+    unsigned long long row[D + 1], pv[D + 1];
+    float4 rj, oj;
     float4 cnew = make_float4(0.f, 0.f, 0.f, 0.f);
     if (j < K) {
-        const size_t o = (size_t)j * (D + 1);
-        unsigned long long pv[D + 1];
-#pragma unroll
-        for (int a = 0; a <= D; ++a) { row[a] = src[o + a]; pv[a] = prev[o + a]; }
-        const float4 rj = cref[(size_t)sel * K + j], oj = C[j];
-#pragma unroll
-        for (int a = 0; a <= D; ++a) neq += (row[a] != pv[a]) ? 1ull : 0ull;   // raw statistics vs the previous ones
-        const unsigned long long c = row[D];
-        float out[4] = {0.f, 0.f, 0.f, 0.f};
-        if (c > 0) {
-#pragma unroll
-            for (int a = 0; a < D; ++a) {
-                const double m = ((double)(long long)row[a] * __builtin_ldexp(1.0, -qe.q[a])) / (double)c;
-                out[a] = (float)m;
-            }
-        } else {
-            ne = 1u;
-        }
-        cnew = make_float4(out[0], out[1], out[2], out[3]);
-#pragma unroll
-        for (int a = 0; a < D; ++a) {
-            const double e1 = (double)comp(cnew, a) - (double)comp(rj, a);
-            const double e2 = (double)comp(cnew, a) - (double)comp(oj, a);
-            dr += e1 * e1;
-            ds += e2 * e2;
-        }
+        upd_load<D>(j, K, src, prev, cref, sel, C, row, pv, rj, oj);
+        upd_row<D>(row, pv, rj, oj, qe, cnew, neq, ne, dr, ds);
         __hip_atomic_store(sh + j, ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // only sh[] is handed to the last block inside this launch: drain it now;
@@ -2594,35 +2688,170 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
         double x = s_tree[lane];
         x = x + s_tree[lane + 64];
         for (int st = 32; st > 0; st >>= 1) x = x + __shfl_down(x, st);   // lane t: x_t + x_{t+st}
-        if (lane == 0) {
-            const double shift = x;
-            const uint32_t it = ctrl->iter;
-            if (it < ctrl->max_iter) {
-                hist_changed[it] = changed;
-                hist_shift[it] = shift;
+        if (lane == 0)
+            upd_publish(ctrl, changed, x, dmax, smax, sel, alpha, dl_cap, hist_changed, hist_shift, ctrl->iter,
+                        ctrl->max_iter, ctrl->budget, ctrl->tol);
+    }
+}
+
+// k_upd in ONE block of SHIFT_LANES threads (K <= UPD1_MAX: configs 1-5): thread L owns centroids L + 1024 r, so its tree lane's
+// sum (ascending r) stays in registers and the halving tree runs in LDS -- no
+// per-block records, no arrival counter, no second pass over sh[] (the
+// multi-block k_upd's hand-off cost ~4 memory latencies: 9.5 us at K = 1024).
+// Same arithmetic, stores and published words as k_upd.
+// R = rows per thread = ceil(K / 1024) (R <= 2 loads both parity halves and
+// both reference buffers speculatively; R = 4 would spill with them).
+constexpr int UPD1_MAX = 4 * SHIFT_LANES;
+template <int D, int R>
+__global__ __launch_bounds__(SHIFT_LANES) void k_upd1(unsigned long long *__restrict__ stats_in,
+                                                      unsigned long long *__restrict__ partials, int K, QExp qe,
+                                                      unsigned long long *__restrict__ held,
+                                                      unsigned long long *__restrict__ prev,
+                                                      const float4 *__restrict__ C, float4 *__restrict__ Cn,
+                                                      const float4 *__restrict__ cref,
+                                                      unsigned long long *__restrict__ hist_changed,
+                                                      double *__restrict__ hist_shift, Ctrl *__restrict__ ctrl,
+                                                      double alpha, double dl_cap) {
+    // every load of the launch in ONE memory latency: the control words, the
+    // rows of both parity halves of `partials` and both reference buffers
+    // (selected once the words are in, instead of a second dependent round)
+    unsigned gate = ctrl->halt | ctrl->done;
+    const uint32_t it = ctrl->iter, max_iter = ctrl->max_iter;
+    const unsigned sel = ctrl->ref_sel;
+    const double budget = ctrl->budget, tol = ctrl->tol;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n = K * (D + 1);
+    // (R > 2: too many registers for both halves -- the rows follow the control
+    // words, one more latency)
+    constexpr bool SPEC = R <= 2;
+    unsigned long long row[R][D + 1], alt[SPEC ? R : 1][D + 1], pv[R][D + 1];
+    float4 rj[R], rk[SPEC ? R : 1], oj[R];
+    const unsigned par = it & 1u;
+    auto load = [&](int r) {
+        const int j = tid + SHIFT_LANES * r;
+        if (j >= K) return;
+        const size_t o = (size_t)j * (D + 1);
+#pragma unroll
+        for (int a = 0; a <= D; ++a) {
+            if constexpr (SPEC) {
+                row[r][a] = stats_in ? stats_in[o + a] : partials[o + a];
+                alt[r][a] = stats_in ? 0ull : partials[(size_t)n + o + a];
+            } else {
+                row[r][a] = stats_in ? stats_in[o + a] : partials[(size_t)par * n + o + a];
             }
-            ctrl->last_changed = changed;
-            ctrl->last_shift = shift;
-            ctrl->resume = 0u;
-            const double slack = 1.0 + 9.094947017729282e-13;   // 1 + 2^-40: fp64 rounding of the drift norms
-            const double budget = ctrl->budget;
-            const bool rebuild = !(sqrt(dmax) * slack <= budget);
-            double dl_new = alpha * sqrt(smax) * slack;
-            if (!(dl_new <= dl_cap)) dl_new = 0.0;
-            if (rebuild) {
-                ctrl->ref_sel = sel ^ 1u;
-                ctrl->budget = dl_new;
-                ctrl->rebuilds += 1u;
-            }
-            ctrl->lists = rebuild ? 2u : 1u;
-            ctrl->lists_dl = rebuild ? dl_new : budget;
-            uint32_t done = 0;
-            if (changed == 0ull) done = 1u;
-            else if (shift <= ctrl->tol) done = 2u;
-            if (!done && it + 1 >= ctrl->max_iter) done = 3u;
-            ctrl->done = done;
-            ctrl->iter = it + 1;
+            pv[r][a] = prev[o + a];
         }
+        if constexpr (SPEC) {
+            rj[r] = cref[j];
+            rk[r] = cref[(size_t)K + j];
+        } else {
+            rj[r] = cref[(size_t)sel * K + j];
+        }
+        oj[r] = C[j];
+    };
+    unsigned long long neq = 0ull;
+    unsigned ne = 0u;
+    double dr = 0.0, ds = 0.0, v = 0.0;
+    float4 cnew[R];
+    auto compute = [&](int r) {
+        const int j = tid + SHIFT_LANES * r;
+        if (j >= K) return;
+        double drj = 0.0, dsj = 0.0;
+        upd_row<D>(row[r], pv[r], rj[r], oj[r], qe, cnew[r], neq, ne, drj, dsj);
+        dr = fmax(dr, drj);
+        ds = fmax(ds, dsj);
+        v = v + dsj;   // tree lane tid: sh[tid + 1024 r] in ascending r
+    };
+    unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
+    // row r's words (each row is read and written by its owning thread only)
+    auto store = [&](int r) {
+        const int j = tid + SHIFT_LANES * r;
+        if (j >= K) return;
+        const size_t o = (size_t)j * (D + 1);
+#pragma unroll
+        for (int a = 0; a <= D; ++a) {
+            prev[o + a] = row[r][a];
+            held[o + a] = row[r][a];   // the relocation snapshot, should this iteration halt
+            pnext[o + a] = 0ull;       // the next accumulation starts from zero
+        }
+        Cn[j] = cnew[r];
+    };
+    if constexpr (SPEC) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) load(r);
+        if (gate != 0u) return;
+        if (!stats_in && par)
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int a = 0; a <= D; ++a) row[r][a] = alt[r][a];
+        if (sel)
+#pragma unroll
+            for (int r = 0; r < R; ++r) rj[r] = rk[r];
+#pragma unroll
+        for (int r = 0; r < R; ++r) compute(r);
+    } else {
+        // the rows follow the control words, in batches of 2 rows (all of them in
+        // flight at once spilled at R = 4)
+        asm volatile("" : "+s"(gate));
+        if (gate != 0u) return;
+#pragma unroll
+        for (int b = 0; b < R; b += 2) {
+            load(b);
+            load(b + 1);
+            compute(b);
+            compute(b + 1);
+            store(b);
+            store(b + 1);
+            asm volatile("" ::: "memory");   // the next batch's loads stay below this one's use
+        }
+    }
+    if constexpr (SPEC)
+#pragma unroll
+        for (int r = 0; r < R; ++r) store(r);
+    if (tid == 0) {
+        held[n] = 0ull;
+        if (stats_in) stats_in[n] = 0ull;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        neq += __shfl_xor(neq, o);
+        ne += __shfl_xor(ne, o);
+        dr = fmax(dr, __shfl_xor(dr, o));
+        ds = fmax(ds, __shfl_xor(ds, o));
+    }
+    constexpr int NW = SHIFT_LANES / 64;
+    __shared__ unsigned long long s_neq[NW];
+    __shared__ unsigned s_ne[NW];
+    __shared__ double s_dr[NW], s_ds[NW];
+    __shared__ double s_tree[SHIFT_LANES];
+    if (lane == 0) { s_neq[wv] = neq; s_ne[wv] = ne; s_dr[wv] = dr; s_ds[wv] = ds; }
+    s_tree[tid] = v;
+    __syncthreads();
+    unsigned long long changed = 0ull, n_empty = 0ull;
+    double dmax = 0.0, smax = 0.0;
+    for (int w = 0; w < NW; ++w) {
+        changed += s_neq[w]; n_empty += s_ne[w]; dmax = fmax(dmax, s_dr[w]); smax = fmax(smax, s_ds[w]);
+    }
+    if (n_empty > 0ull) {   // empty cluster: the host relocates, then k_global + k_cand resume
+        if (tid == 0) {
+            ctrl->n_empty = (unsigned)n_empty;
+            ctrl->neq_saved = changed;
+            ctrl->lists = 0u;
+            ctrl->halt = 1u;
+        }
+        return;
+    }
+    // the halving tree of oracle/lloyd_ref.py shift_total: lane L += lane L + h
+    for (int h = SHIFT_LANES / 2; h >= 64; h >>= 1) {
+        if (tid < h) s_tree[tid] = s_tree[tid] + s_tree[tid + h];
+        __syncthreads();
+    }
+    if (wv == 0) {
+        double x = s_tree[lane];
+        for (int st = 32; st > 0; st >>= 1) x = x + __shfl_down(x, st);   // lane t: x_t + x_{t+st}
+        if (lane == 0)
+            upd_publish(ctrl, changed, x, dmax, smax, sel, alpha, dl_cap, hist_changed, hist_shift, it, max_iter,
+                        budget, tol);
     }
 }
 
@@ -2642,10 +2871,18 @@ __global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__rest
     unsigned mode = ctrl->lists;
     unsigned sel = ctrl->ref_sel;
     double dl = ctrl->lists_dl;
+    // STAGE: all K new centres staged in LDS by one coalesced pass, issued with
+    // the control-word loads (one memory latency for both; a gated launch
+    // leaves the LDS copy unused): the list phases' reads of them (references,
+    // tests, compaction) become LDS reads instead of dependent global round trips
+    extern __shared__ __attribute__((aligned(16))) float4 cstage[];
+    if constexpr (STAGE)
+        for (int j = threadIdx.x; j < K; j += CAND_TPB) cstage[j] = Cn[j];
     asm volatile("" : "+s"(halt), "+s"(mode), "+s"(sel), "+s"(dl));
     if (halt != 0u || mode == 0u) return;
+    if constexpr (STAGE) __syncthreads();
     for (int j = blockIdx.x * CAND_TPB + threadIdx.x; j < K; j += gridDim.x * CAND_TPB) {
-        const float4 c = Cn[j];
+        const float4 c = STAGE ? cstage[j] : Cn[j];
         C[j] = c;
         if (mode == 2u) cref[(size_t)sel * K + j] = c;
     }
@@ -2653,17 +2890,167 @@ __global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__rest
         refresh_body<D>(g, Cn, fc_cnt, fc_rec, fc_lab);
         return;
     }
-    if constexpr (STAGE) {
-        // all K new centres staged in LDS by one coalesced pass: the list phases'
-        // reads of them (references, tests, compaction) become LDS reads instead
-        // of dependent global round trips
-        extern __shared__ __attribute__((aligned(16))) float4 cstage[];
-        for (int j = threadIdx.x; j < K; j += CAND_TPB) cstage[j] = Cn[j];
-        __syncthreads();
-        cand_body<D, FC>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
-    } else {
-        cand_body<D, FC>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+    if constexpr (STAGE) cand_body<D, FC>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+    else cand_body<D, FC>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+}
+
+// Centre update and candidate lists in ONE launch (D <= 3, K <= CAND_TPB * 2 =
+// 1024: configs 1-4).  Every block loads all K statistics rows (both parity
+// halves of `partials`, or the all-reduced buffer), the previous rows, the old
+// centres and both reference buffers together with the control words -- one
+// memory latency -- and computes all K new centres into LDS plus the
+// order-independent decisions every block needs identically (an empty cluster
+// halts; the largest drift and shift give rebuild-or-refresh and the new
+// budget).  Then one agent-scope arrival per block; the LAST block to arrive
+// (every other block's loads have returned by then) publishes what k_upd does
+// -- prev, held, the zeroed next accumulation target, C and the new reference
+// buffer, the shift tree of oracle/lloyd_ref.py shift_total, history and flags
+// -- and every block rebuilds or refreshes its own cells' lists from the LDS
+// centres.  Replaces k_upd1 + k_lists (two launches, ~16 us at an 8-way slab).
+template <int D, int R>
+__global__ __launch_bounds__(CAND_TPB) void k_updlists(
+    unsigned long long *__restrict__ stats_in, unsigned long long *__restrict__ partials, int K, QExp qe,
+    unsigned long long *__restrict__ held, unsigned long long *__restrict__ prev, float4 *__restrict__ C,
+    float4 *__restrict__ cref, unsigned long long *__restrict__ hist_changed, double *__restrict__ hist_shift,
+    Ctrl *__restrict__ ctrl, double alpha, double dl_cap, Grid g, uint32_t *__restrict__ fc_cnt,
+    float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab, int bpc) {
+    static_assert(R * CAND_TPB <= SHIFT_LANES && SHIFT_LANES % CAND_TPB == 0, "one tree lane per row");
+    extern __shared__ __attribute__((aligned(16))) float4 cstage[];   // the K new centres
+    unsigned gate = ctrl->halt | ctrl->done;
+    const uint32_t it = ctrl->iter, max_iter = ctrl->max_iter;
+    const unsigned sel = ctrl->ref_sel;
+    const double budget = ctrl->budget, tol = ctrl->tol;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n = K * (D + 1);
+    // row r of this thread: centroid j = tid + CAND_TPB * r (tree lane j)
+    unsigned long long row[R][D + 1], alt[R][D + 1], pv[R][D + 1];
+    float4 rj[R], rk[R], oj[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int j = tid + CAND_TPB * r;
+        if (j < K) {
+            const size_t o = (size_t)j * (D + 1);
+#pragma unroll
+            for (int a = 0; a <= D; ++a) {
+                row[r][a] = stats_in ? stats_in[o + a] : partials[o + a];
+                alt[r][a] = stats_in ? 0ull : partials[(size_t)n + o + a];
+                pv[r][a] = prev[o + a];
+            }
+            rj[r] = cref[j];
+            rk[r] = cref[(size_t)K + j];
+            oj[r] = C[j];
+        }
     }
+    if (gate != 0u) return;
+    const unsigned par = it & 1u;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!stats_in && par)
+#pragma unroll
+            for (int a = 0; a <= D; ++a) row[r][a] = alt[r][a];
+        if (sel) rj[r] = rk[r];
+    }
+    unsigned long long neq = 0ull;
+    unsigned ne = 0u;
+    double dr = 0.0, ds = 0.0, sh[R];
+    float4 cnew[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int j = tid + CAND_TPB * r;
+        sh[r] = 0.0;
+        if (j < K) {
+            double drj = 0.0, dsj = 0.0;
+            upd_row<D>(row[r], pv[r], rj[r], oj[r], qe, cnew[r], neq, ne, drj, dsj);
+            dr = fmax(dr, drj);
+            ds = fmax(ds, dsj);
+            sh[r] = dsj;
+            cstage[j] = cnew[r];
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        neq += __shfl_xor(neq, o);
+        ne += __shfl_xor(ne, o);
+        dr = fmax(dr, __shfl_xor(dr, o));
+        ds = fmax(ds, __shfl_xor(ds, o));
+    }
+    constexpr int NW = CAND_TPB / 64;
+    __shared__ unsigned long long s_neq[NW];
+    __shared__ unsigned s_ne[NW];
+    __shared__ double s_dr[NW], s_ds[NW];
+    __shared__ unsigned s_last;
+    if (lane == 0) { s_neq[wv] = neq; s_ne[wv] = ne; s_dr[wv] = dr; s_ds[wv] = ds; }
+    __syncthreads();   // every load of this block has returned (its values are used above)
+    if (tid == 0) {
+        const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prior == gridDim.x - 1) ? 1u : 0u;
+    }
+    unsigned long long changed = 0ull, n_empty = 0ull;
+    double dmax = 0.0, smax = 0.0;
+    for (int w = 0; w < NW; ++w) {
+        changed += s_neq[w]; n_empty += s_ne[w]; dmax = fmax(dmax, s_dr[w]); smax = fmax(smax, s_ds[w]);
+    }
+    // the decisions of upd_publish, identical in every block (same data, order-free maxima)
+    const double slack = 1.0 + 9.094947017729282e-13;
+    const bool rebuild = !(sqrt(dmax) * slack <= budget);
+    double dl_new = alpha * sqrt(smax) * slack;
+    if (!(dl_new <= dl_cap)) dl_new = 0.0;
+    __syncthreads();   // s_last
+    if (s_last) {
+        // ---- the publisher: every other block's loads have returned
+        unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int j = tid + CAND_TPB * r;
+            if (j < K) {
+                const size_t o = (size_t)j * (D + 1);
+#pragma unroll
+                for (int a = 0; a <= D; ++a) {
+                    prev[o + a] = row[r][a];
+                    held[o + a] = row[r][a];   // the relocation snapshot, should this iteration halt
+                    pnext[o + a] = 0ull;       // the next accumulation starts from zero
+                }
+                if (n_empty == 0ull) {         // a halted iteration leaves C (the relocation needs it)
+                    C[j] = cnew[r];
+                    if (rebuild) cref[(size_t)(sel ^ 1u) * K + j] = cnew[r];
+                }
+            }
+        }
+        if (tid == 0) {
+            held[n] = 0ull;
+            if (stats_in) stats_in[n] = 0ull;
+            __hip_atomic_store(&ctrl->u_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (n_empty > 0ull) {
+            if (tid == 0) {
+                ctrl->n_empty = (unsigned)n_empty;
+                ctrl->neq_saved = changed;
+                ctrl->lists = 0u;
+                ctrl->halt = 1u;
+            }
+        } else {
+            // tree lane L < 1024 holds sh[L] (K <= 1024); the first halving step
+            // (lane t += lane t + 512) runs in this thread's registers
+            static_assert(CAND_TPB == SHIFT_LANES / 2, "thread t holds tree lanes t and t + 512");
+            __shared__ double s_tree[CAND_TPB];
+            s_tree[tid] = sh[0] + (R > 1 ? sh[R > 1 ? 1 : 0] : 0.0);
+            __syncthreads();
+            for (int h = SHIFT_LANES / 4; h >= 64; h >>= 1) {
+                if (tid < h) s_tree[tid] = s_tree[tid] + s_tree[tid + h];
+                __syncthreads();
+            }
+            if (wv == 0) {
+                double x = s_tree[lane];
+                for (int st = 32; st > 0; st >>= 1) x = x + __shfl_down(x, st);   // lane t: x_t + x_{t+st}
+                if (lane == 0)
+                    upd_publish(ctrl, changed, x, dmax, smax, sel, alpha, dl_cap, hist_changed, hist_shift, it,
+                                max_iter, budget, tol);
+            }
+        }
+    }
+    if (n_empty > 0ull) return;   // halted: the lists stay (resume rebuilds them)
+    // this block's cells: rebuilt at the new centres with the new budget, or refreshed
+    if (rebuild) cand_body<D, 4>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new, CoarseL{});
+    else refresh_body<D>(g, cstage, fc_cnt, fc_rec, fc_lab);
 }
 
 // ------------------------------------------------------------------ relocation

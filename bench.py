@@ -238,39 +238,43 @@ def slab_proxy(args) -> dict:
         e.begin(C0, 0.0, iters + 4)
         engines.append(e)
     del Xp
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(P)]
+    # one event set per timed step, read after the last one: the queue never runs
+    # dry between steps (a per-step synchronize let the first engine's start event
+    # fire before the host had submitted its kernel -- the round-3 "first-engine
+    # artefact", ~8 us)
+    ev = [[[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(P)] for _ in range(args.steps)]
     t_assign = np.zeros(P)
     t_step = np.zeros(P)
 
-    def step(timed):
+    def step(evs):
         for r, e in enumerate(engines):
-            if timed:
-                ev[r][0].record()
+            if evs:
+                evs[r][0].record()
             e.iter_local()
-            if timed:
-                ev[r][1].record()
+            if evs:
+                evs[r][1].record()
         total = engines[0].stats.clone()
         for e in engines[1:]:
             total += e.stats
         for e in engines:
             e.stats.copy_(total)
         for r, e in enumerate(engines):
-            if timed:
-                ev[r][2].record()
+            if evs:
+                evs[r][2].record()
             e.iter_global()
-            if timed:
-                ev[r][3].record()
-        if timed:
-            torch.cuda.synchronize()
-            for r in range(P):
-                t_assign[r] += ev[r][0].elapsed_time(ev[r][1])
-                t_step[r] += ev[r][2].elapsed_time(ev[r][3])
+            if evs:
+                evs[r][3].record()
 
     for _ in range(args.warmup):
-        step(False)
+        step(None)
     torch.cuda.synchronize()
-    for _ in range(args.steps):
-        step(True)
+    for k in range(args.steps):
+        step(ev[k])
+    torch.cuda.synchronize()
+    for k in range(args.steps):
+        for r in range(P):
+            t_assign[r] += ev[k][r][0].elapsed_time(ev[k][r][1])
+            t_step[r] += ev[k][r][2].elapsed_time(ev[k][r][3])
     st = [e.status() for e in engines]
     if any(s["halt"] or s["iter"] != iters for s in st):
         raise SystemExit(f"slab proxy: iterations did not all run: {st[0]}")

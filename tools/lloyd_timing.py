@@ -1,19 +1,38 @@
 """Calibration (debug build -DPCM_DBG_TIMING): per-block phase times of the
-k_lloyd launch of the last of `iters` iterations.
-usage: python tools/lloyd_timing.py SO_PATH [iters] [N K D]  (default config 3)"""
+k_lloyd1 launch of the last of `iters` iterations.
+usage: python tools/lloyd_timing.py SO_PATH [iters] [N K D [f16] [slab P]]  (default config 3)
+  slab P: time rank 0's spatial slab of a P-way split (the layout bench.py --slab-of P
+  and the multi-GPU run use) instead of a whole-cloud engine"""
 import ctypes, os, sys
 import numpy as np
 os.environ["PCM_SO"] = sys.argv[1]
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pcm_amd import lloyd, _lib
-from pcm_amd.engine import Engine, synth_rows, synth_uniform
-N, K, D = (int(v) for v in sys.argv[3:6]) if len(sys.argv) > 5 else (100_000_000, 1024, 3)
+from pcm_amd.engine import Engine, shard_hist, shard_partition, synth_rows, synth_uniform
+from pcm_amd.fixed import fixed_q
+rest = sys.argv[3:]
+N, K, D = (int(v) for v in rest[:3]) if len(rest) >= 3 else (100_000_000, 1024, 3)
+pdt = torch.float16 if "f16" in rest else torch.float32
+P = int(rest[rest.index("slab") + 1]) if "slab" in rest else 1
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-X = synth_uniform(N, D, seed=0, start=0)
-C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0)
-eng = Engine(D, K, torch.float32, max_iter=50)
-lloyd.prepare(eng, X, None)
+X = synth_uniform(N, D, seed=0, start=0).to(pdt)
+C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0).to(pdt).float()
+eng = Engine(D, K, pdt, max_iter=50)
+if P > 1:   # rank 0's slab, built as bench.slab_proxy does
+    lo, hi, maxabs = Engine(D, K, pdt, max_iter=1).bbox(X)
+    q = fixed_q(maxabs)
+    axis = int(np.argmax(hi - lo))
+    inv = lloyd.SLAB_BINS / (hi[axis] - lo[axis])
+    owner = lloyd.slab_owner(shard_hist(X, axis, lo[axis], inv, lloyd.SLAB_BINS).cpu().numpy(), P)
+    Xp, rows, cnt = shard_partition(X, axis, lo[axis], inv, lloyd.SLAB_BINS, owner, P, 0)
+    Xr, rr = Xp[:int(cnt[0])].contiguous(), rows[:int(cnt[0])].contiguous()
+    del X, Xp
+    eng.bbox(Xr)
+    eng.set_shard(rr, N)
+    eng.build(Xr, q, 0)
+else:
+    lloyd.prepare(eng, X, None)
 eng.begin(C0, 0.0, 50)
 eng.iterate(iters); torch.cuda.synchronize()
 lib = _lib.load()
@@ -25,7 +44,10 @@ t = buf.astype(np.int64)
 t = t[t[:, 0] > 0]
 t0 = t[:, 0].min()
 us = lambda v: np.asarray(v) / 100.0   # s_memrealtime: 100 MHz
-print(f"N={N} K={K} D={D} blocks {len(t)} kernel span {us(t[:, 3].max() - t0):.1f} us")
+info = eng.layout_info()
+print(f"N={N} K={K} D={D} {pdt} slab {P} (rank 0: {int(eng.n)} points, cells {info['ncells']}, tiles "
+      f"{info['ntiles']}, kernel {eng.assign_kernel()}, lists {eng.candidate_stats()}) blocks {len(t)} "
+      f"kernel span {us(t[:, 3].max() - t0):.1f} us")
 for name, a, b in (("start (rel. first)", None, 0), ("setup (start->first round)", 0, 1), ("rounds", 1, 2),
                    ("fold+exit", 2, 3), ("block total", 0, 3), ("end (rel. first start)", None, 3)):
     v = t[:, b] - (t0 if a is None else t[:, a])
