@@ -1063,7 +1063,10 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
             for (int a = 0; a < D; ++a)
                 if (e->g.ext[a] > 0 && (wmin == 0.0 || e->g.w[a] < wmin)) wmin = e->g.w[a];
             // D <= 3, K <= 1024: update and lists in one launch (k_updlists)
-            static const bool fused_on = [] { const char *v = std::getenv("PCM_FUSED_UPD"); return v && std::atoi(v) != 0; }();
+            // (PCM_FUSED_UPD=0: k_upd1 + k_lists instead -- A/B and tests; read per
+            // launch so tests can switch it between fits, captured graphs keep theirs)
+            const char *fz = std::getenv("PCM_FUSED_UPD");
+            const bool fused_on = !(fz && std::atoi(fz) == 0);
             if (fused_on && D <= 3 && !split_coarse(e) && e->k <= 2 * CAND_TPB) {
                 const int bpc = cand_bpc(e);
                 auto fused = [&](auto RR) {
@@ -1086,10 +1089,8 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
             };
             if (e->k <= SHIFT_LANES)
                 upd1(std::integral_constant<int, 1>{});
-            else if (e->k <= 2 * SHIFT_LANES)
-                upd1(std::integral_constant<int, 2>{});
             else if (e->k <= UPD1_MAX)
-                upd1(std::integral_constant<int, 4>{});
+                upd1(std::integral_constant<int, 2>{});
             else
                 k_upd<D><<<blocks_for(e->k, UPD_TPB), UPD_TPB, 0, s>>>(
                     from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->Cn,

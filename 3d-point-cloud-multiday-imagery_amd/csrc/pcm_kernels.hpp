@@ -368,13 +368,10 @@ __device__ __forceinline__ unsigned zwidth(unsigned span) { return span ? 32u - 
 #ifndef PCM_ZWAVE
 #define PCM_ZWAVE 1
 #endif
-// Record fields: x = bits [0, w0), y = [w0, w0 + w1), z = the top w2 bits
-// (PCM_ZTOP, default: x by a mask, y by one funnel shift of the two words, z by
-// one shift of the high word -- 7 VALU per point) or z = [w0 + w1, w0 + w1 + w2)
-// (PCM_ZTOP=0: two 64-bit shifts, ~11 VALU per point).
-#ifndef PCM_ZTOP
-#define PCM_ZTOP 1
-#endif
+// Record fields: x = bits [0, w0), y = [w0, w0 + w1), z = the top w2 bits (x by
+// a mask, y by one funnel shift of the two words, z by one shift of the high
+// word: 7 VALU per point; z after y took two 64-bit shifts, ~11 VALU, and
+// measured ~1.5 % slower per k_lloyd1 launch at config 3, profiles/rd4_ztop_ab.txt).
 #if PCM_ZWAVE
 constexpr unsigned ZHI = 256;
 __host__ __device__ __forceinline__ size_t zword(size_t i) { return (i >> 8) * 512u + (i & 255u); }
@@ -443,7 +440,7 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
         // the z field sits at the top of the 64-bit record (decoded by one shift of
         // the high word): at least 1 bit wide, so the shift stays below 32
         // (w0 + w1 <= 62: the extra bit always fits)
-        if (PCM_ZTOP && w[2] == 0u) { w[2] = 1u; ++total; }
+        if (w[2] == 0u) { w[2] = 1u; ++total; }
         ok = ok && total <= 64u;
         meta = make_uint4(lo[0], lo[1], lo[2], ok ? (0x80000000u | w[0] | (w[1] << 8) | (w[2] << 16)) : 0u);
         tmeta[t] = meta;
@@ -460,7 +457,7 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
         const unsigned long long d0 = bits[u][0] - m.x;
         const unsigned long long d1 = bits[u][1] - m.y;
         const unsigned long long d2 = bits[u][2] - m.z;
-        const unsigned long long v = d0 | (d1 << w0) | (d2 << (PCM_ZTOP ? 64u - w2 : w0 + w1));
+        const unsigned long long v = d0 | (d1 << w0) | (d2 << (64u - w2));
         const size_t g = zword(i);
         xz[g] = (unsigned)v;
         xz[g + ZHI] = (unsigned)(v >> 32);
@@ -1260,23 +1257,17 @@ __device__ __forceinline__ void load_z2(R &r, rsrc_t rA, unsigned off_pt) {
     r.w[4] = v1[0]; r.w[5] = v1[1]; r.w[6] = v1[2]; r.w[7] = v1[3];
 }
 // exact fp32 coordinates of a compressed item (k_tile_compress): base + delta bits
-// (sh1 = w0; sh2 = 32 - w2 with PCM_ZTOP, else w0 + w1)
+// (sh1 = w0, sh2 = 32 - w2)
 template <typename R, int DD>
 __device__ __forceinline__ void unpack_z(const R &r, float (&x)[4][DD], const uint4 &zm, unsigned sh1,
-                                         unsigned sh2, unsigned m0, unsigned m1, unsigned m2) {
+                                         unsigned sh2, unsigned m0, unsigned m1) {
     static_assert(DD == 3 && sizeof(r.w) >= 8 * sizeof(unsigned), "compressed tiles: fp32 D = 3");
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const unsigned lo = r.w[e], hi = r.w[4 + e];
         x[e][0] = __uint_as_float(zm.x + (lo & m0));
-#if PCM_ZTOP
         x[e][1] = __uint_as_float(zm.y + (__builtin_amdgcn_alignbit(hi, lo, sh1) & m1));
         x[e][2] = __uint_as_float(zm.z + (hi >> sh2));
-#else
-        const unsigned long long v = ((unsigned long long)hi << 32) | lo;
-        x[e][1] = __uint_as_float(zm.y + ((unsigned)(v >> sh1) & m1));
-        x[e][2] = __uint_as_float(zm.z + ((unsigned)(v >> sh2) & m2));
-#endif
     }
 }
 // AoSoA-4 (xs_index): word a*4 + e holds coordinate a of the lane's point e
@@ -1869,8 +1860,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     // compressed tile (k_tile_compress): 8-B records from xz, decoded exactly
     const bool zc = ZOK && (zm.w >> 31);
     const unsigned zw0 = zm.w & 0xffu, zw1 = (zm.w >> 8) & 0xffu, zw2 = (zm.w >> 16) & 0xffu;
-    const unsigned zsh1 = zw0, zsh2 = PCM_ZTOP ? 32u - zw2 : zw0 + zw1;
-    const unsigned zm0 = (1u << zw0) - 1u, zm1 = (1u << zw1) - 1u, zm2 = (1u << zw2) - 1u;
+    const unsigned zsh1 = zw0, zsh2 = 32u - zw2;
+    const unsigned zm0 = (1u << zw0) - 1u, zm1 = (1u << zw1) - 1u;
     const unsigned bpp = zc ? 8u : (unsigned)(D * sizeof(T));
     const rsrc_t rA = make_rsrc(zc ? (const void *)A.xz : A.xs, (unsigned long long)(zc ? (A.npad + 255) / 256 * 256 : A.npad) * bpp);
     // lanes past the tile's end get the out-of-range offset: zeros, no memory traffic
@@ -1964,7 +1955,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
                     Raw<float, 3> raw;
                     if (zc) {
                         load_z2(raw, rA, off);
-                        unpack_z(raw, x, zm, zsh1, zsh2, zm0, zm1, zm2);
+                        unpack_z(raw, x, zm, zsh1, zsh2, zm0, zm1);
                     } else {
                         load_x<float, 3>(raw, rxf, off);
                         unpack_x<3>(raw, x);
@@ -2151,7 +2142,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         const unsigned rbase = base0 + (unsigned)r * 4u * TPB;
         const unsigned i0 = rbase + 4u * tid;
         float x[4][D];
-        if constexpr (ZC) unpack_z(cx, x, zm, zsh1, zsh2, zm0, zm1, zm2);
+        if constexpr (ZC) unpack_z(cx, x, zm, zsh1, zsh2, zm0, zm1);
         else unpack_x<D>(cx, x);
         int bj[4];
         if (mm == 1) {
@@ -2694,14 +2685,15 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
     }
 }
 
-// k_upd in ONE block of SHIFT_LANES threads (K <= UPD1_MAX: configs 1-5): thread L owns centroids L + 1024 r, so its tree lane's
+// k_upd in ONE block of SHIFT_LANES threads (K <= UPD1_MAX: configs 1-4): thread L owns centroids L + 1024 r, so its tree lane's
 // sum (ascending r) stays in registers and the halving tree runs in LDS -- no
 // per-block records, no arrival counter, no second pass over sh[] (the
 // multi-block k_upd's hand-off cost ~4 memory latencies: 9.5 us at K = 1024).
 // Same arithmetic, stores and published words as k_upd.
-// R = rows per thread = ceil(K / 1024) (R <= 2 loads both parity halves and
-// both reference buffers speculatively; R = 4 would spill with them).
-constexpr int UPD1_MAX = 4 * SHIFT_LANES;
+// R = rows per thread = ceil(K / 1024).  K = 4096 (config 5) keeps the
+// multi-block k_upd: one block doing 4 rows per thread (in batches, to stay
+// within 128 VGPRs) measured 28 us against k_upd's 15 at an 8-way config-5 slab.
+constexpr int UPD1_MAX = 2 * SHIFT_LANES;
 template <int D, int R>
 __global__ __launch_bounds__(SHIFT_LANES) void k_upd1(unsigned long long *__restrict__ stats_in,
                                                       unsigned long long *__restrict__ partials, int K, QExp qe,
@@ -2723,92 +2715,64 @@ __global__ __launch_bounds__(SHIFT_LANES) void k_upd1(unsigned long long *__rest
     const int n = K * (D + 1);
     // (R > 2: too many registers for both halves -- the rows follow the control
     // words, one more latency)
-    constexpr bool SPEC = R <= 2;
-    unsigned long long row[R][D + 1], alt[SPEC ? R : 1][D + 1], pv[R][D + 1];
-    float4 rj[R], rk[SPEC ? R : 1], oj[R];
+    static_assert(R >= 1 && R <= 2, "K <= UPD1_MAX");
+    unsigned long long row[R][D + 1], alt[R][D + 1], pv[R][D + 1];
+    float4 rj[R], rk[R], oj[R];
     const unsigned par = it & 1u;
-    auto load = [&](int r) {
-        const int j = tid + SHIFT_LANES * r;
-        if (j >= K) return;
-        const size_t o = (size_t)j * (D + 1);
 #pragma unroll
-        for (int a = 0; a <= D; ++a) {
-            if constexpr (SPEC) {
+    for (int r = 0; r < R; ++r) {
+        const int j = tid + SHIFT_LANES * r;
+        if (j < K) {
+            const size_t o = (size_t)j * (D + 1);
+#pragma unroll
+            for (int a = 0; a <= D; ++a) {
                 row[r][a] = stats_in ? stats_in[o + a] : partials[o + a];
                 alt[r][a] = stats_in ? 0ull : partials[(size_t)n + o + a];
-            } else {
-                row[r][a] = stats_in ? stats_in[o + a] : partials[(size_t)par * n + o + a];
+                pv[r][a] = prev[o + a];
             }
-            pv[r][a] = prev[o + a];
-        }
-        if constexpr (SPEC) {
             rj[r] = cref[j];
             rk[r] = cref[(size_t)K + j];
-        } else {
-            rj[r] = cref[(size_t)sel * K + j];
+            oj[r] = C[j];
         }
-        oj[r] = C[j];
-    };
+    }
+    if (gate != 0u) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!stats_in && par)
+#pragma unroll
+            for (int a = 0; a <= D; ++a) row[r][a] = alt[r][a];
+        if (sel) rj[r] = rk[r];
+    }
     unsigned long long neq = 0ull;
     unsigned ne = 0u;
     double dr = 0.0, ds = 0.0, v = 0.0;
     float4 cnew[R];
-    auto compute = [&](int r) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
         const int j = tid + SHIFT_LANES * r;
-        if (j >= K) return;
-        double drj = 0.0, dsj = 0.0;
-        upd_row<D>(row[r], pv[r], rj[r], oj[r], qe, cnew[r], neq, ne, drj, dsj);
-        dr = fmax(dr, drj);
-        ds = fmax(ds, dsj);
-        v = v + dsj;   // tree lane tid: sh[tid + 1024 r] in ascending r
-    };
-    unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
-    // row r's words (each row is read and written by its owning thread only)
-    auto store = [&](int r) {
-        const int j = tid + SHIFT_LANES * r;
-        if (j >= K) return;
-        const size_t o = (size_t)j * (D + 1);
-#pragma unroll
-        for (int a = 0; a <= D; ++a) {
-            prev[o + a] = row[r][a];
-            held[o + a] = row[r][a];   // the relocation snapshot, should this iteration halt
-            pnext[o + a] = 0ull;       // the next accumulation starts from zero
-        }
-        Cn[j] = cnew[r];
-    };
-    if constexpr (SPEC) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) load(r);
-        if (gate != 0u) return;
-        if (!stats_in && par)
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int a = 0; a <= D; ++a) row[r][a] = alt[r][a];
-        if (sel)
-#pragma unroll
-            for (int r = 0; r < R; ++r) rj[r] = rk[r];
-#pragma unroll
-        for (int r = 0; r < R; ++r) compute(r);
-    } else {
-        // the rows follow the control words, in batches of 2 rows (all of them in
-        // flight at once spilled at R = 4)
-        asm volatile("" : "+s"(gate));
-        if (gate != 0u) return;
-#pragma unroll
-        for (int b = 0; b < R; b += 2) {
-            load(b);
-            load(b + 1);
-            compute(b);
-            compute(b + 1);
-            store(b);
-            store(b + 1);
-            asm volatile("" ::: "memory");   // the next batch's loads stay below this one's use
+        if (j < K) {
+            double drj = 0.0, dsj = 0.0;
+            upd_row<D>(row[r], pv[r], rj[r], oj[r], qe, cnew[r], neq, ne, drj, dsj);
+            dr = fmax(dr, drj);
+            ds = fmax(ds, dsj);
+            v = v + dsj;   // tree lane tid: sh[tid + 1024 r] in ascending r
         }
     }
-    if constexpr (SPEC)
+    unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
 #pragma unroll
-        for (int r = 0; r < R; ++r) store(r);
+    for (int r = 0; r < R; ++r) {
+        const int j = tid + SHIFT_LANES * r;
+        if (j < K) {
+            const size_t o = (size_t)j * (D + 1);
+#pragma unroll
+            for (int a = 0; a <= D; ++a) {
+                prev[o + a] = row[r][a];
+                held[o + a] = row[r][a];   // the relocation snapshot, should this iteration halt
+                pnext[o + a] = 0ull;       // the next accumulation starts from zero
+            }
+            Cn[j] = cnew[r];
+        }
+    }
     if (tid == 0) {
         held[n] = 0ull;
         if (stats_in) stats_in[n] = 0ull;

@@ -329,3 +329,22 @@ def test_engine_reserve(pcm):
     with pytest.raises(PcmError):
         eng.iterate(1)
     eng.close()
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_update_paths(pcm, fused, monkeypatch):
+    """The centre update + list paths (k_upd1 + k_lists, or the fused k_updlists
+    behind PCM_FUSED_UPD=1) against the oracle: list rebuilds and refreshes,
+    an empty cluster (halt, relocation, resume) and tol convergence."""
+    monkeypatch.setenv("PCM_FUSED_UPD", fused)
+    X = R.splitmix_uniform(120_000, 3, 31)
+    for k, iters, tol in ((1024, 12, 0.0), (700, 10, 0.0), (64, 40, 1e-6)):
+        C0 = X[R.init_indices(X.shape[0], k)]
+        ref = R.lloyd_fit(X, C0, max_iter=iters, tol=tol, fast=True)
+        assert_same(gpu_fit(pcm, X, C0, iters, tol=tol), ref, f"fused={fused} k={k}")
+    # relocation: duplicated initial centres leave clusters empty
+    Xr = R.splitmix_uniform(50_000, 3, 32)
+    C0 = Xr[R.init_indices(50_000, 200)].copy()
+    C0[100:150] = C0[0]
+    ref = R.lloyd_fit(Xr, C0, max_iter=15, fast=True)
+    assert_same(gpu_fit(pcm, Xr, C0, 15), ref, f"fused={fused} relocation")
