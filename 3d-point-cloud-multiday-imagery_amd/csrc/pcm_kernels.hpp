@@ -2844,6 +2844,7 @@ __global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__rest
         for (int j = threadIdx.x; j < K; j += CAND_TPB) cstage[j] = Cn[j];
     asm volatile("" : "+s"(halt), "+s"(mode), "+s"(sel), "+s"(dl));
     if (halt != 0u || mode == 0u) return;
+    DBG_T(0);
     if constexpr (STAGE) __syncthreads();
     for (int j = blockIdx.x * CAND_TPB + threadIdx.x; j < K; j += gridDim.x * CAND_TPB) {
         const float4 c = STAGE ? cstage[j] : Cn[j];
