@@ -1104,8 +1104,14 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
                 CoarseL cl;
                 cl.in_cnt = e->cl_cnt;
                 cl.in_idx = e->cl_idx;
-                k_lists<D, 2><<<(int)n_mid(e), CAND_TPB, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl, e->fc_cnt,
-                                                                  e->fc_rec, e->fc_lab, 1, cl);
+                // mid-cell blocks of 256 threads (PCM_LISTS4_TPB=512: the round-4 start's size, A/B only)
+                const char *lt = std::getenv("PCM_LISTS4_TPB");
+                if (lt && std::atoi(lt) == 512)
+                    k_lists<D, 2><<<(int)n_mid(e), CAND_TPB, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl,
+                                                                      e->fc_cnt, e->fc_rec, e->fc_lab, 1, cl);
+                else
+                    k_lists<D, 2, false, 256><<<(int)n_mid(e), 256, 0, s>>>(e->g, e->Cn, e->C, e->cref, e->k, e->ctrl,
+                                                                             e->fc_cnt, e->fc_rec, e->fc_lab, 1, cl);
             } else if (e->k <= LISTS_STAGE_MAX) {   // centres staged in LDS
                 const int bpc = cand_bpc(e);
                 k_lists<D, 4, true><<<(int)(e->g.ncoarse * bpc), CAND_TPB, (size_t)e->k * sizeof(float4), s>>>(

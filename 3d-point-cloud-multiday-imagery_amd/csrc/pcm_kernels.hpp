@@ -702,7 +702,7 @@ struct CoarseL {
 // FC = 2: a mid cell (2^D children, D = 4 layouts) whose list REFINES its
 // coarse parent's k_coarse list -- the same exact test against the mid box --
 // so the fine lists prune ~2^D-times shorter lists than the coarse ones.
-template <int D, int FC = 4>
+template <int D, int FC = 4, int TPB = CAND_TPB>
 __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K, uint32_t *__restrict__ fc_cnt,
                                           float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab, int BPC,
                                           double dl = 0.0, CoarseL cl = CoarseL{}) {
@@ -737,12 +737,12 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
 
     // ---- 1. this block's cell list
     if (cl.in_cnt && !refine) {   // computed by k_coarse for this iteration's centres
-        for (int w = tid; w < CAND_CBW; w += CAND_TPB) cbits[w] = 0ull;
+        for (int w = tid; w < CAND_CBW; w += TPB) cbits[w] = 0ull;
         if (tid == 0) s_mp = cl.in_cnt[I];
         __syncthreads();
         const uint32_t m0 = s_mp;
         if (m0 != FULL)
-            for (uint32_t l = tid; l < m0; l += CAND_TPB) {
+            for (uint32_t l = tid; l < m0; l += TPB) {
                 const int j = cl.in_idx[(size_t)I * CAP + l];
                 pidx[l] = j;
                 prec[l] = C[j];
@@ -765,22 +765,22 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
             if (m0 != FULL) {
                 nsrc = (int)m0;
                 from_list = true;
-                for (int l = tid; l < nsrc; l += CAND_TPB) sidx[l] = cl.in_idx[(size_t)Ipar * CAP + l];
+                for (int l = tid; l < nsrc; l += TPB) sidx[l] = cl.in_idx[(size_t)Ipar * CAP + l];
             }
         }
         auto src = [&](int p) -> int { return from_list ? sidx[p] : p; };
         const bool bitmap = nsrc <= CAND_KBITS;
         if (tid == 0) rkey = ~0ull;
         if (bitmap)
-            for (int w = tid; w < CAND_KBITS / 64; w += CAND_TPB) kbits[w] = 0ull;
-        for (int w = tid; w < CAND_CBW; w += CAND_TPB) cbits[w] = 0ull;
+            for (int w = tid; w < CAND_KBITS / 64; w += TPB) kbits[w] = 0ull;
+        for (int w = tid; w < CAND_CBW; w += TPB) cbits[w] = 0ull;
         __syncthreads();
         // reference key: fp32 bits of the max distance (any centre is a valid
         // reference; the key only ranks them) with the low 11 bits replaced by
         // j's wave-local rank -> per-wave DPP minimum, then one LDS atomic per wave
         uint32_t best = ~0u;
         int bjj = 0;
-        for (int p = tid; p < nsrc; p += CAND_TPB) {
+        for (int p = tid; p < nsrc; p += TPB) {
             const int j = src(p);
             const float m = (float)maxdist<D>(blo, bhi, C[j]);
             if (__float_as_uint(m) < best) { best = __float_as_uint(m); bjj = j; }
@@ -795,7 +795,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         if (bitmap) {
             // a wave's 64 consecutive source positions fill one bitmap word: a
             // ballot and a plain store (no 64-way contended LDS atomic)
-            for (int p0 = 0; p0 < nsrc; p0 += CAND_TPB) {
+            for (int p0 = 0; p0 < nsrc; p0 += TPB) {
                 const int p = p0 + tid;
                 const bool keep = p < nsrc && !prunable<D>(blo, bhi, C[src(p < nsrc ? p : 0)], r, dl, mr);
                 const unsigned long long bal = __ballot(keep);
@@ -820,7 +820,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                 if (lane == 63) s_mp = x <= (uint32_t)CAP ? x : FULL;
             }
             __syncthreads();
-            for (int w = wv; w < nwk; w += CAND_TPB / 64) {
+            for (int w = wv; w < nwk; w += TPB / 64) {
                 const unsigned long long word = kbits[w];
                 const uint32_t pos = wpre[w] + __popcll(word & ((1ull << lane) - 1ull));
                 if (((word >> lane) & 1ull) && pos < (uint32_t)CAP) {
@@ -830,10 +830,10 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                 }
             }
         } else {
-            // large K: ordered compaction by ballots (one barrier pair per CAND_TPB centres)
-            __shared__ uint32_t wcnt[CAND_TPB / 64];
+            // large K: ordered compaction by ballots (one barrier pair per TPB centres)
+            __shared__ uint32_t wcnt[TPB / 64];
             uint32_t total = 0;
-            for (int base = 0; base < nsrc; base += CAND_TPB) {
+            for (int base = 0; base < nsrc; base += TPB) {
                 const int p = base + tid;
                 const int j = src(p < nsrc ? p : 0);
                 const bool keep = p < nsrc && !prunable<D>(blo, bhi, C[j], r, dl, mr);
@@ -847,7 +847,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
                     prec[pos] = C[j];
                     pidx[pos] = j;
                 }
-                for (int w = 0; w < CAND_TPB / 64; ++w) total += wcnt[w];
+                for (int w = 0; w < TPB / 64; ++w) total += wcnt[w];
                 __syncthreads();
             }
             if (tid == 0) s_mp = total <= (uint32_t)CAP ? total : FULL;
@@ -861,7 +861,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     if (cl.out_cnt) {   // k_coarse: publish the coarse list, no children
         if (tid == 0) cl.out_cnt[I] = mp;
         if (!pfull)
-            for (uint32_t l = tid; l < mp; l += CAND_TPB) cl.out_idx[(size_t)I * CAP + l] = pidx[l];
+            for (uint32_t l = tid; l < mp; l += TPB) cl.out_idx[(size_t)I * CAP + l] = pidx[l];
         return;
     }
     if (pfull) mp = (uint32_t)K;
@@ -875,7 +875,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     // other (100M: 64 children per block, 15 -> 9.6 us); with few children per
     // block (12.5M shard: 8) the wave path's two chains per wave are shorter
     // (mid blocks, FC = 2: 16 children over lists of tens to hundreds: the pair path too)
-    if (!pfull && ((c1 - c0) >= 2 * CAND_TPB / 16 || FC == 2) && (c1 - c0) <= CAND_MAXCH &&
+    if (!pfull && ((c1 - c0) >= 2 * TPB / 16 || FC == 2) && (c1 - c0) <= CAND_MAXCH &&
         (c1 - c0) * nwc <= CAND_CBW) {
         // Pair path: one thread per (child, coarse-list position) in three
         // block-wide passes -- (A) reference = a parent candidate nearest the
@@ -885,7 +885,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         // lists equal the wave path's; all pairs run in parallel instead of one
         // child per wave after another (100M: 15 -> ~2 us per block).
         const int nch = c1 - c0, npair = nch * (int)mp;
-        const int dch = CAND_TPB / (int)mp, dlp = CAND_TPB % (int)mp;
+        const int dch = TPB / (int)mp, dlp = TPB % (int)mp;
         constexpr uint32_t LM = CAP > 256 ? 0x3FFu : 0xFFu;
         // (0) per-child cell id, fp64 box and centre, once per child
         __shared__ double s_blo[CAND_MAXCH][D], s_bhi[CAND_MAXCH][D];
@@ -893,7 +893,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         __shared__ long long s_cell[CAND_MAXCH];
         __shared__ float4 s_ref[CAND_MAXCH];   // the child's reference centre (pass A)
         __shared__ double s_mr[CAND_MAXCH];    // max distance from the child's box to it (drift budget > 0)
-        for (int ch = tid; ch < nch; ch += CAND_TPB) {
+        for (int ch = tid; ch < nch; ch += TPB) {
             int f[MAXD];
             bool inside = true;
 #pragma unroll
@@ -918,7 +918,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         // an LDS atomic per pair serialised ~25-way on the child's word)
         {
             int tpc = 64;
-            while (tpc > 1 && tpc * nch > CAND_TPB) tpc >>= 1;
+            while (tpc > 1 && tpc * nch > TPB) tpc >>= 1;
             const int ch = tid / tpc, sub = tid % tpc;
             uint32_t best = ~0u;
             if (ch < nch && s_cell[ch] >= 0)
@@ -957,9 +957,9 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         // (B) keep bits; the lanes of one (child, bitmap word) are contiguous in a
         // wave, so one ballot and one LDS atomic per segment
         {
-            const int iters = (npair + CAND_TPB - 1) / CAND_TPB;
+            const int iters = (npair + TPB - 1) / TPB;
             int ch = tid / (int)mp, l = tid % (int)mp;
-            for (int it = 0, p = tid; it < iters; ++it, p += CAND_TPB) {
+            for (int it = 0, p = tid; it < iters; ++it, p += TPB) {
                 bool keep = false;
                 const bool valid = p < npair && s_cell[ch < nch ? ch : 0] >= 0 && ch < nch;
                 if (valid) {
@@ -983,7 +983,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
         __syncthreads();
         DBG_T(12);
         // (C)
-        for (int p = tid, ch = tid / (int)mp, l = tid % (int)mp; p < npair; p += CAND_TPB) {
+        for (int p = tid, ch = tid / (int)mp, l = tid % (int)mp; p < npair; p += TPB) {
             const long long cell = s_cell[ch];
             if (cell >= 0) {
                 const unsigned long long *wb = cbits + ch * nwc;
@@ -1013,7 +1013,7 @@ __device__ __forceinline__ void cand_body(const Grid &g, const float4 *C, int K,
     // wave path (FULL parent, or more pairs than the LDS bitmaps hold): one wave per child cell
     auto child = [&](auto PFc) {
         constexpr bool PF = decltype(PFc)::value;
-        for (int ch = c0 + wv; ch < c1; ch += CAND_TPB / 64) {
+        for (int ch = c0 + wv; ch < c1; ch += TPB / 64) {
             int f[MAXD];
             bool inside = true;
 #pragma unroll
@@ -1137,10 +1137,10 @@ __global__ __launch_bounds__(CAND_TPB) void k_coarse(Grid g, const float4 *__res
 // Candidate records refreshed to the new centres (lists still valid under the
 // drift budget): every fine cell's records, grid-stride over the cells with 16
 // threads per cell, every load of a cell's count and ids issued in parallel.
-template <int D>
+template <int D, int TPB = CAND_TPB>
 __device__ __forceinline__ void refresh_body(const Grid &g, const float4 *cn, const uint32_t *__restrict__ fc_cnt,
                                              float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab) {
-    constexpr int PER = 16, CPB = CAND_TPB / PER;   // threads per cell, cells per block pass
+    constexpr int PER = 16, CPB = TPB / PER;   // threads per cell, cells per block pass
     const int sub = (int)threadIdx.x % PER;
     for (long long cell = (long long)blockIdx.x * CPB + (int)threadIdx.x / PER; cell < g.ncells;
          cell += (long long)gridDim.x * CPB) {
@@ -2826,8 +2826,8 @@ __global__ __launch_bounds__(SHIFT_LANES) void k_upd1(unsigned long long *__rest
 // centres); queued no-op launches after convergence repeat the same copy and
 // lists (idempotent).
 constexpr int LISTS_STAGE_MAX = 2048;   // k_lists stages the centres in LDS up to this K (32 KB)
-template <int D, int FC = 4, bool STAGE = false>
-__global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__restrict__ Cn, float4 *__restrict__ C,
+template <int D, int FC = 4, bool STAGE = false, int TPB = CAND_TPB>
+__global__ __launch_bounds__(TPB) void k_lists(Grid g, const float4 *__restrict__ Cn, float4 *__restrict__ C,
                                                     float4 *__restrict__ cref, int K, const Ctrl *__restrict__ ctrl,
                                                     uint32_t *__restrict__ fc_cnt, float4 *__restrict__ fc_rec,
                                                     int32_t *__restrict__ fc_lab, int bpc, CoarseL cl) {
@@ -2841,22 +2841,22 @@ __global__ __launch_bounds__(CAND_TPB) void k_lists(Grid g, const float4 *__rest
     // tests, compaction) become LDS reads instead of dependent global round trips
     extern __shared__ __attribute__((aligned(16))) float4 cstage[];
     if constexpr (STAGE)
-        for (int j = threadIdx.x; j < K; j += CAND_TPB) cstage[j] = Cn[j];
+        for (int j = threadIdx.x; j < K; j += TPB) cstage[j] = Cn[j];
     asm volatile("" : "+s"(halt), "+s"(mode), "+s"(sel), "+s"(dl));
     if (halt != 0u || mode == 0u) return;
     DBG_T(0);
     if constexpr (STAGE) __syncthreads();
-    for (int j = blockIdx.x * CAND_TPB + threadIdx.x; j < K; j += gridDim.x * CAND_TPB) {
+    for (int j = blockIdx.x * TPB + threadIdx.x; j < K; j += gridDim.x * TPB) {
         const float4 c = STAGE ? cstage[j] : Cn[j];
         C[j] = c;
         if (mode == 2u) cref[(size_t)sel * K + j] = c;
     }
     if (mode != 2u) {
-        refresh_body<D>(g, Cn, fc_cnt, fc_rec, fc_lab);
+        refresh_body<D, TPB>(g, Cn, fc_cnt, fc_rec, fc_lab);
         return;
     }
-    if constexpr (STAGE) cand_body<D, FC>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
-    else cand_body<D, FC>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+    if constexpr (STAGE) cand_body<D, FC, TPB>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
+    else cand_body<D, FC, TPB>(g, Cn, K, fc_cnt, fc_rec, fc_lab, bpc, dl, cl);
 }
 
 // Centre update and candidate lists in ONE launch (D <= 3, K <= CAND_TPB * 2 =
