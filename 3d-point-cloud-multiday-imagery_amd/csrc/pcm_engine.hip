@@ -349,8 +349,12 @@ void choose_grid(pcm_engine *e) {
     // D = 4: smaller cells (~1k points) shorten the lists more than the tiles
     // cost (config-5 shape: 20736 -> 65536 cells, 913 -> 846 us per iteration)
     // (a spatial shard holds about n / n_global of the centres: the cap scales with it)
+    // D = 4 slabs: 48 cells per centre (config-5 8-way slab, 13718 -> 27783 cells,
+    // lists 7.1 -> 5.3, one tile per cell: 280 -> 250 us per rank; 36501 cells 265,
+    // profiles/rd4_c5_slab_grid.txt); D <= 3: 32 (the config-4 slab sweep)
     const double share = e->n_global > 0 ? std::min(1.0, (double)e->n / (double)e->n_global) : 1.0;
-    double target = std::min(32.0 * e->k * share, (double)e->n / (e->d >= 4 ? 1000.0 : 2800.0));
+    const double per_centre = e->d >= 4 ? 48.0 : 32.0;
+    double target = std::min(per_centre * e->k * share, (double)e->n / (e->d >= 4 ? 1000.0 : 2800.0));
     if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     make_grid(e->g, e->d, e->lo, e->hi, target);
     if (e->k <= 1) e->g.prune = 0;
