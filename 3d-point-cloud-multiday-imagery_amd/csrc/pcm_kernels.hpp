@@ -1431,7 +1431,8 @@ __global__ void k_inert_fold(unsigned long long *__restrict__ rep, unsigned long
 // E-step with the current centres writing labels (sorted order) and the
 // inertia (final E-step of _kmeans.py:736-750, relocation keys).  Not gated.
 // Same tile walk and candidate lists as k_lloyd; 4 points per lane per round,
-// the loads of the next round in flight while one is computed.
+// the loads of the next round in flight while one is computed; compressed
+// tiles read their 8-B records (round 4), like k_lloyd1.
 template <typename T, int D, typename LT>
 __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned long long *inert_out, int iscale) {
     __shared__ float4 crec[CAPF];
@@ -1443,6 +1444,9 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned 
     const int32_t *llab = A.fc_lab;
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     const rsrc_t rl = make_rsrc(lab, (unsigned long long)A.npad * sizeof(LT));
+    constexpr bool ZOK = sizeof(T) == 4 && D == 3;   // compressed tiles exist only for fp32 D = 3
+    const rsrc_t rz = make_rsrc(A.xz ? (const void *)A.xz : A.xs,
+                                A.xz ? (unsigned long long)(A.npad + 255) / 256 * 256 * 8 : 0ull);
     unsigned long long ilo = 0ull, ihi = 0ull;
     unsigned iovf = 0u;
     for (unsigned t = blockIdx.x; t < nt; t += G) {
@@ -1461,32 +1465,53 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned 
         }
         TileL h = make_tile(tr, A.K);
         if (glab) { h.full = 1; h.mm = (int)tr.w; }
+        // compressed tile (fp32 D = 3): its 8-B records, decoded exactly as in k_lloyd1
+        uint4 zm = make_uint4(0u, 0u, 0u, 0u);
+        if (ZOK && A.tmeta) zm = A.tmeta[t];
         __syncthreads();
         if (!h.full && tid < h.mm) {
             crec[tid] = trec[tid];
             cid[tid] = tlab[tid];
         }
         __syncthreads();
-        Raw<T, D> cur, nxt;
-        LOAD_X(cur, h.base0 + 4u * tid);
-        for (int r = 0; r < h.nr; ++r) {
-            const unsigned i0 = h.base0 + (unsigned)r * 4u * TPB + 4u * tid;
-            LOAD_X(nxt, r + 1 < h.nr ? i0 + 4u * TPB : 0x0ffffff0u);
-            float x[4][D];
-            unpack_x<D>(cur, x);
-            float bd[4];
-            int bj[4];
-            if (h.full) scan4<D>(Cs, h.mm, x, bd, bj);
-            else scan4<D>(crec, h.mm, x, bd, bj);
-            int lbl[4];
-            bool v[4];
-            for (int e = 0; e < 4; ++e) {
-                lbl[e] = h.full ? (glab ? glab[bj[e]] : bj[e]) : cid[bj[e]];
-                v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
-                if (v[e] && inert_out) inert_add(ilo, ihi, iovf, bd[e], iscale);
+        // one instance per point format (block-uniform per tile), so each keeps a
+        // constant load count per item for hipcc's waitcnt pass
+        auto run = [&](auto ZCc) {
+            constexpr bool ZC = decltype(ZCc)::value;
+            const unsigned zw0 = zm.w & 0xffu, zw1 = (zm.w >> 8) & 0xffu, zw2 = (zm.w >> 16) & 0xffu;
+            const unsigned zsh1 = zw0, zsh2 = 32u - zw2, zm0 = (1u << zw0) - 1u, zm1 = (1u << zw1) - 1u;
+            auto ldx = [&](Raw<T, D> &dst, unsigned off) {
+                if constexpr (ZC) load_z2(dst, rz, off);
+                else load_x<T, D>(dst, rx, off);
+            };
+            Raw<T, D> cur, nxt;
+            ldx(cur, h.base0 + 4u * tid);
+            for (int r = 0; r < h.nr; ++r) {
+                const unsigned i0 = h.base0 + (unsigned)r * 4u * TPB + 4u * tid;
+                ldx(nxt, r + 1 < h.nr ? i0 + 4u * TPB : 0x0ffffff0u);
+                float x[4][D];
+                if constexpr (ZC) unpack_z(cur, x, zm, zsh1, zsh2, zm0, zm1);
+                else unpack_x<D>(cur, x);
+                float bd[4];
+                int bj[4];
+                if (h.full) scan4<D>(Cs, h.mm, x, bd, bj);
+                else scan4<D>(crec, h.mm, x, bd, bj);
+                int lbl[4];
+                bool v[4];
+                for (int e = 0; e < 4; ++e) {
+                    lbl[e] = h.full ? (glab ? glab[bj[e]] : bj[e]) : cid[bj[e]];
+                    v[e] = (i0 + e >= h.start) && (i0 + e < h.end);
+                    if (v[e] && inert_out) inert_add(ilo, ihi, iovf, bd[e], iscale);
+                }
+                if (i0 < h.end) store_l4(rl, i0, lbl, v, (RawLab<LT> *)nullptr);
+                cur = nxt;
             }
-            if (i0 < h.end) store_l4(rl, i0, lbl, v, (RawLab<LT> *)nullptr);
-            cur = nxt;
+        };
+        if constexpr (ZOK) {
+            if (zm.w >> 31) run(std::true_type{});
+            else run(std::false_type{});
+        } else {
+            run(std::false_type{});
         }
     }
     if (inert_out) inert_flush(ilo, ihi, iovf, inert_out);
