@@ -1323,10 +1323,18 @@ int pcm_labels(pcm_engine *e, int32_t *out, void *stream) {
             // sorted -> between the passes -> caller rows
             if (ensure(e->ws, e->cap_ws, (size_t)e->n * sizeof(LT) + 64) != hipSuccess)
                 return fail(PCM_E_NOMEM, "labels scratch");
-            LT *mid = (LT *)e->ws;
-            k_lab_gather<LT><<<blocks_for(e->n), 256, 0, s>>>(e->dmap + e->n, (const LT *)e->lab, e->n, mid);
+            LT *mid = (LT *)e->ws;   // 256-B aligned scratch
+            const uint32_t *m1 = e->dmap + e->n;   // the second pass's map: 16-B aligned iff n % 4 == 0
+            const int g4 = (int)blocks_for((e->n + 3) / 4);
+            if (((uintptr_t)m1 & 15u) == 0)
+                k_lab_gather4<LT, LT, true, true><<<g4, 256, 0, s>>>(m1, (const LT *)e->lab, e->n, mid);
+            else
+                k_lab_gather4<LT, LT, false, true><<<g4, 256, 0, s>>>(m1, (const LT *)e->lab, e->n, mid);
             LAUNCHCHK();
-            k_lab_gather_i32<LT><<<blocks_for(e->n), 256, 0, s>>>(e->dmap, mid, e->n, out);
+            if (a16)
+                k_lab_gather4<LT, int32_t, true, true><<<g4, 256, 0, s>>>(e->dmap, mid, e->n, out);
+            else
+                k_lab_gather4<LT, int32_t, true, false><<<g4, 256, 0, s>>>(e->dmap, mid, e->n, out);
             LAUNCHCHK();
             return 0;
         }

@@ -279,18 +279,41 @@ __global__ __launch_bounds__(256) void k_cell_starts_xs(const T *__restrict__ xs
 // maps (dmap_q: input position of pass q -> its output position), one gather
 // per pass from the last to the first: a pass's outputs are runs of its input
 // order, so the gathers read runs instead of single random words.
-template <typename LT>
-__global__ __launch_bounds__(256) void k_lab_gather(const uint32_t *__restrict__ dmap, const LT *__restrict__ src,
-                                                    long long n, LT *__restrict__ dst) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i < n) dst[i] = src[dmap[i]];
-}
-
-template <typename LT>
-__global__ __launch_bounds__(256) void k_lab_gather_i32(const uint32_t *__restrict__ dmap, const LT *__restrict__ src,
-                                                        long long n, int32_t *__restrict__ out) {
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i < n) out[i] = (int32_t)src[dmap[i]];
+// 4 consecutive outputs per thread: the map as one 16-B load
+// (VM: the map is 16-B aligned) and the outputs as one 8-B / 16-B store (VO:
+// the destination is aligned), the 4 run-wise source reads in flight together
+// (one output per thread moved ~1.9 TB/s: two dependent 2-B accesses a lane).
+template <typename LT, typename OT, bool VM, bool VO>
+__global__ __launch_bounds__(256) void k_lab_gather4(const uint32_t *__restrict__ dmap, const LT *__restrict__ src,
+                                                     long long n, OT *__restrict__ dst) {
+    const long long i4 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * 4;
+    if (i4 >= n) return;
+    if (i4 + 4 > n) {
+        for (long long i = i4; i < n; ++i) dst[i] = (OT)src[dmap[i]];
+        return;
+    }
+    uint32_t m[4];
+    if constexpr (VM) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(dmap + i4);
+        m[0] = v.x; m[1] = v.y; m[2] = v.z; m[3] = v.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] = dmap[i4 + k];
+    }
+    OT o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (OT)src[m[k]];
+    if constexpr (VO && sizeof(OT) == 2) {
+        uint2 w;
+        w.x = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
+        w.y = (uint32_t)(uint16_t)o[2] | ((uint32_t)(uint16_t)o[3] << 16);
+        *reinterpret_cast<uint2 *>(dst + i4) = w;
+    } else if constexpr (VO && sizeof(OT) == 4) {
+        *reinterpret_cast<int4 *>(dst + i4) = make_int4((int)o[0], (int)o[1], (int)o[2], (int)o[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[i4 + k] = o[k];
+    }
 }
 
 // xs padding [n, npad): zeros
