@@ -348,3 +348,19 @@ def test_update_paths(pcm, fused, monkeypatch):
     C0[100:150] = C0[0]
     ref = R.lloyd_fit(Xr, C0, max_iter=15, fast=True)
     assert_same(gpu_fit(pcm, Xr, C0, 15), ref, f"fused={fused} relocation")
+
+
+def test_update_paths_d4(pcm):
+    """D = 4 update paths (k_upd1 for K <= 2048, else k_upd; k_coarse, then the
+    256-thread k_lists<4, 2>) against the oracle: list rebuilds, fp16 points,
+    an empty cluster."""
+    fused = "-"
+    X = R.splitmix_uniform(160_000, 4, 41).astype(np.float16).astype(np.float32)
+    for k, iters in ((300, 10), (3000, 6)):
+        C0 = X[R.init_indices(X.shape[0], k)]
+        ref = R.lloyd_fit(X, C0, max_iter=iters, fast=True)
+        assert_same(gpu_fit(pcm, X, C0, iters, dtype=torch.float16), ref, f"fused={fused} d4 k={k}")
+    C0 = X[R.init_indices(X.shape[0], 120)].copy()
+    C0[60:90] = C0[0]
+    ref = R.lloyd_fit(X, C0, max_iter=8, fast=True)
+    assert_same(gpu_fit(pcm, X, C0, 8, dtype=torch.float16), ref, f"fused={fused} d4 relocation")
