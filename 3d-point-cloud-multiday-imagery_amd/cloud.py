@@ -50,6 +50,10 @@ def assemble_cloud_device(disparity, validity=None, max_disp: int = MAX_DISP):
                                       _ptr(pts), _ptr(hn), ctypes.byref(m), normal.ctypes.data_as(ctypes.c_void_p),
                                       _stream()), "pcm_cloud_assemble")
     M = int(m.value)
-    if M == 0:
-        raise ValueError("no valid disparity pixels")
+    if M < 3:
+        # the reference's plane fit takes ``Vh[2]`` of the thin SVD of the (M, 3)
+        # centred points (plugin.py:164-165), which has min(M, 3) rows: fewer than
+        # 3 valid pixels raise numpy's IndexError there, and the run becomes one
+        # "Error: <msg>" layer (plugin.py:236-241) -- same exception, same text
+        raise IndexError(f"index 2 is out of bounds for axis 0 with size {M}")
     return pts[:M], hn[:M], normal

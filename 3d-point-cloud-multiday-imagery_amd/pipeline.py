@@ -110,10 +110,12 @@ def pair_layers(pp: PairProducts, points: np.ndarray, h_norm: np.ndarray) -> lis
     height = np.full((H, W), np.nan)
     height[y, x] = h_norm                      # normalise_for_display(height_map, valid) at valid pixels
     layers = [(height, {"name": f"{PREFIX} Disparity", "colormap": "turbo", "scale": (1, 1)}, "image")]
-    valid = pp.photoconsistency > 0            # plugin.py:194
-    layers.append((normalise_for_display(pp.photoconsistency, valid) if valid.any() else
-                   np.zeros((H, W)), {"name": f"{PREFIX} Photoconsistency", "colormap": "turbo", "scale": (1, 1)},
-                   "image"))
+    valid = pp.photoconsistency > 0            # plugin.py:195
+    # no positive photoconsistency: np.percentile of an empty selection raises
+    # IndexError inside normalise_for_display (utils.py:12 via plugin.py:196), as
+    # in the reference, and the run becomes its "Error: <msg>" layer
+    layers.append((normalise_for_display(pp.photoconsistency, valid),
+                   {"name": f"{PREFIX} Photoconsistency", "colormap": "turbo", "scale": (1, 1)}, "image"))
     layers.append(((~valid).astype(np.float32), {"name": f"{PREFIX} Invalid Mask", "colormap": MASK_COLORMAP,
                                                    "scale": (1, 1), "contrast_limits": [0, 1]}, "image"))
     layers.append((points, {"name": f"{PREFIX} 3D Point Cloud", "size": 2, "properties": {"height": h_norm},

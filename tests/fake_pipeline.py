@@ -62,8 +62,11 @@ class SyntheticStages:
     (disparity, validity mask, photoconsistency, debug image layers) of the
     shape the reference's disparity_map returns (disparity.py:21-226)."""
 
-    def __init__(self, n_pairs=2, shape=(120, 160), seed=0, fail_at=None, fail=None):
+    def __init__(self, n_pairs=2, shape=(120, 160), seed=0, fail_at=None, fail=None, n_valid=None, dark_at=None):
         self.n_pairs, self.shape, self.seed, self.fail_at, self.fail = n_pairs, shape, seed, fail_at, fail
+        # n_valid = (pair, m): that pair keeps only its first m valid pixels (row-major);
+        # dark_at = pair whose photoconsistency is nowhere positive
+        self.n_valid, self.dark_at = n_valid, dark_at
         self.logged = []
 
     def log(self, msg):
@@ -85,6 +88,12 @@ class SyntheticStages:
             disparity[rng.random((H, W)) < 0.02] = 16.0 * 1000           # WLS sentinel
             validity = rng.random((H, W)) > 0.1
             photo = np.where(rng.random((H, W)) < 0.8, rng.uniform(0, 0.3, (H, W)), 0.0)
+            if self.n_valid is not None and self.n_valid[0] == p:
+                validity = np.zeros((H, W), bool)
+                validity.flat[:self.n_valid[1]] = True
+                disparity.flat[:self.n_valid[1]] = -16.0 * (1.0 + np.arange(self.n_valid[1]))   # in range
+            if self.dark_at == p:
+                photo = np.zeros((H, W))
             image_layers = [(rng.random((H, W)), {"name": f"{PREFIX} Input Left", "colormap": "gray"}, "image")] \
                 if is_debug_mode else []
             yield PairProducts(disparity=disparity, validity=validity, photoconsistency=photo,
