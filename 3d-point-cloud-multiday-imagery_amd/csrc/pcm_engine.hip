@@ -430,7 +430,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->bbox_part, (size_t)BBOX_BLOCKS * 2 * MAXD * sizeof(float));
     err = err ? err : hipMalloc(&e->nonfinite, sizeof(unsigned));
     err = err ? err : hipMalloc(&e->bbox_out, 2 * MAXD * sizeof(double));
-    err = err ? err : hipMalloc(&e->cand_stats, 3 * sizeof(unsigned long long));
+    err = err ? err : hipMalloc(&e->cand_stats, 6 * sizeof(unsigned long long));
     err = err ? err : hipMalloc(&e->empty_idx, (size_t)k * sizeof(int));
     err = err ? err : hipMalloc(&e->ntiles_dev, 2 * sizeof(uint32_t));
     err = err ? err : hipMalloc(&e->zpts, 32 * 16 * sizeof(unsigned long long));
@@ -1469,7 +1469,7 @@ int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *crowded_tiles, int64_
     *crowded_tiles = *listed_tiles = *listed_len = 0;
     if (e->zlev <= 0 || e->n == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipMemsetAsync(e->cand_stats, 0, 3 * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(e->cand_stats, 0, 6 * sizeof(unsigned long long), s));
     k_tile_list_stats<<<blocks_for(e->ntiles_cap), 256, 0, s>>>(e->tiles, e->ntiles_dev, e->fc_cnt, e->tl_cnt,
                                                                  e->cand_stats);
     LAUNCHCHK();
@@ -1479,6 +1479,25 @@ int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *crowded_tiles, int64_
     *crowded_tiles = (int64_t)h[0];
     *listed_tiles = (int64_t)h[1];
     *listed_len = (int64_t)h[2];
+    return 0;
+}
+
+int pcm_tile_list_detail(pcm_engine *e, int64_t *long_lists, int64_t *allk_tiles, int64_t *max_len, void *stream) {
+    if (!e || !long_lists || !allk_tiles || !max_len) return fail(PCM_E_ARG, "bad argument");
+    if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
+    *long_lists = *allk_tiles = *max_len = 0;
+    if (e->zlev <= 0 || e->n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(e->cand_stats, 0, 6 * sizeof(unsigned long long), s));
+    k_tile_list_stats<<<blocks_for(e->ntiles_cap), 256, 0, s>>>(e->tiles, e->ntiles_dev, e->fc_cnt, e->tl_cnt,
+                                                                 e->cand_stats);
+    LAUNCHCHK();
+    unsigned long long h[6];
+    HIPCHK(hipMemcpyAsync(h, e->cand_stats, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *long_lists = (int64_t)h[3];
+    *allk_tiles = (int64_t)h[4];
+    *max_len = (int64_t)h[5];
     return 0;
 }
 

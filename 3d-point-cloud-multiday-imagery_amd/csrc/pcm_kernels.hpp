@@ -612,7 +612,9 @@ __global__ __launch_bounds__(256) void k_tile_cand(const uint4 *__restrict__ til
 }
 
 // Tile-list summary: out[0] += tiles of cells past TL_MIN, out[1] += those with a
-// tile list, out[2] += the lengths of those lists.
+// tile list, out[2] += the lengths of those lists; out[3] += tile lists longer
+// than TLCAP (k_lloyd1 scans them through LDS chunks), out[4] += all-K tiles (a
+// FULL cell whose tile got no list either), out[5] = the longest tile list.
 __global__ __launch_bounds__(256) void k_tile_list_stats(const uint4 *__restrict__ tiles,
                                                          const uint32_t *__restrict__ ntiles,
                                                          const uint32_t *__restrict__ fc_cnt,
@@ -620,12 +622,17 @@ __global__ __launch_bounds__(256) void k_tile_list_stats(const uint4 *__restrict
                                                          unsigned long long *__restrict__ out) {
     const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (t >= *ntiles) return;
-    if (fc_cnt[tiles[t].x] <= TL_MIN) return;
+    const uint32_t cc = fc_cnt[tiles[t].x];
+    if (cc <= TL_MIN) return;
     atomicAdd(out, 1ull);
     const uint32_t c = tl_cnt[t];
     if (c != FULL) {
         atomicAdd(out + 1, 1ull);
         atomicAdd(out + 2, (unsigned long long)c);
+        if (c > (uint32_t)TLCAP) atomicAdd(out + 3, 1ull);
+        atomicMax(out + 5, (unsigned long long)c);
+    } else if (cc == FULL) {
+        atomicAdd(out + 4, 1ull);
     }
 }
 

@@ -224,6 +224,10 @@ class Engine:
         if z.value > 0:   # crowded layout: tiles of long-list / FULL cells and their own lists
             out.update(zlev=z.value, crowded_tiles=ft.value, listed_tiles=lt.value,
                        tile_list_mean=(ll.value / lt.value) if lt.value else 0.0)
+            lg, ak, ml = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            _lib.check(self.lib.pcm_tile_list_detail(self.h, ctypes.byref(lg), ctypes.byref(ak), ctypes.byref(ml),
+                                                     _stream()), "pcm_tile_list_detail")
+            out.update(long_tile_lists=lg.value, allk_tiles=ak.value, tile_list_max=ml.value)
         return out
 
 

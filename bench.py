@@ -72,6 +72,48 @@ def cpu_baseline(X, C, budget_s: float = 12.0) -> dict:
                       f"(-O3 -ffp-contract=off, OpenMP {threads} threads, {cpu_model})"}
 
 
+def numpy_baseline(X, C, budget_s: float = 6.0) -> dict:
+    """The NumPy restatement (oracle/lloyd_ref.py local_stats: chunked direct-form
+    distances, argmin, exact int64 accumulation -- the Python-level cost of the
+    reference-style CPU path, BASELINE.md "CPU-baseline plan") timed on a leading
+    subsample of the bench cloud, one E-step + accumulation pass over it, grown
+    until the pass takes about budget_s / 4."""
+    from oracle import lloyd_ref as R
+
+    n_all, d = X.shape
+    k = C.shape[0]
+    q = R.fixed_q(X)
+    m = min(n_all, 16384)
+    while True:
+        Xs = np.ascontiguousarray(X[:m])
+        t0 = time.perf_counter()
+        R.local_stats(Xs, C, np.full(m, -1, np.int32), q)
+        dt = time.perf_counter() - t0
+        if dt >= budget_s / 4 or m >= n_all:
+            break
+        m = min(n_all, m * 4)
+    return {"value": m / dt, "unit": "point·iters/s", "cores": 1, "kind": "port",
+            "sample": f"1 E-step + exact accumulation over the first {m} points of the bench cloud, K={k}, "
+                      f"D={d}, oracle/lloyd_ref.py NumPy path (single process)"}
+
+
+def cpu_fit_baseline(X, C, iters: int) -> dict:
+    """Config 2 ('full run on both CPU and GPU'): the whole
+    `iters`-iteration fit by oracle/lloyd_ref.c (OpenMP, all granted cores), plus
+    its result for the GPU parity check."""
+    from oracle import lloyd_ref as R
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    t0 = time.perf_counter()
+    ref = R.lloyd_fit(X, C, max_iter=iters, tol=0.0, fast=True)
+    dt = time.perf_counter() - t0
+    n = X.shape[0]
+    return {"value": n * ref["n_iter"] / dt, "unit": "point·iters/s", "cores": threads, "kind": "port",
+            "fit_ms": dt * 1e3,
+            "sample": f"the whole {ref['n_iter']}-iteration fit (+ final E-step) of all {n} points, K={C.shape[0]}, "
+                      f"oracle/lloyd_ref.c brute force (OpenMP {threads} threads)"}, ref
+
+
 def cloud_bench(H: int = 4000, W: int = 4000) -> dict:
     """Per-pair cloud assembly (plugin.py:147-192) of a synthetic HxW disparity:
     GPU (pcm_amd.assemble_cloud, host arrays in and out, like the plugin) vs the
@@ -165,6 +207,27 @@ def pmc_traffic(n, k, d, world):
     if rd is None or wr is None:
         return None, None
     return rd + wr, os.path.relpath(path, ROOT)
+
+
+FP32_PEAK_TFLOPS = 157.3       # MI355X vector FP32 (MI355X_MICROARCH.md; f32 MFMA runs at the same rate)
+
+
+def compute_roofline(n: int, k: int, d: int, cand_mean: float, launch_ms: float) -> dict:
+    """The assign kernel against the FP32 compute roofline (BASELINE.md "Reported per
+    config"): (3D + 1) flop per point and candidate (D subtractions, D squares, D - 1
+    additions, one compare) over the candidates actually scanned (the mean list
+    length; the uniform cloud's cells hold equal point counts), and the brute-force
+    equivalent over all K centres (what the pruning saves; above 1 means the pruned
+    kernel beats a brute-force kernel running at peak)."""
+    if launch_ms <= 0:
+        return None
+    fpc = 3 * d + 1
+    t = launch_ms * 1e-3
+    done = n * cand_mean * fpc / t / 1e12
+    brute = n * k * fpc / t / 1e12
+    return {"bound": "fp32 valu", "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "flop_per_point_candidate": fpc,
+            "candidates_per_point": cand_mean, "achieved": done, "compute_frac": done / FP32_PEAK_TFLOPS,
+            "bruteforce_equivalent": brute, "bruteforce_equivalent_frac": brute / FP32_PEAK_TFLOPS}
 
 
 def _free_port() -> int:
@@ -338,9 +401,17 @@ def main():
     ap.add_argument("--clustered", type=int, default=0, metavar="C",
                     help="degenerate-cloud check: C tight Gaussian clusters (sigma 0.004) + 1%% uniform background "
                          "instead of the uniform cloud (pruning stress: FULL candidate lists, long lists)")
+    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5],
+                    help="BASELINE.json config preset: 2 = N=1M K=64 D=3 f32, 20 timed iterations, GPU and CPU "
+                         "whole 20-iteration fits with a bitwise parity check; 3/4 = the defaults (4: run with "
+                         "--gpus N); 5 = N=500M K=4096 D=4 f16 (needs >= 2 GPUs: 2^28 points per engine)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher test: each rank prints its RANK/WORLD_SIZE as JSON and exits before any GPU call")
     args = ap.parse_args()
+    if args.config == 2:
+        args.n, args.k, args.d, args.dtype, args.steps = 1_000_000, 64, 3, "f32", 20
+    elif args.config == 5:
+        args.n, args.k, args.d, args.dtype = 500_000_000, 4096, 4, "f16"
 
     env_world = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and env_world is None:
@@ -428,13 +499,21 @@ def main():
     layout_ms = (time.perf_counter() - t0) * 1e3
     eng.begin(C0, 0.0, max_iter)
 
-    def iterate(n):
+    ar_events = []
+
+    def iterate(n, record=False):
         if not multi:
             eng.iterate(n)
         else:
             for _ in range(n):
                 eng.iter_local()
+                if record:   # HIP events around the collective on the launch stream (RCCL's stream joins it)
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record()
                 dist.all_reduce(eng.stats)
+                if record:
+                    ev[1].record()
+                    ar_events.append(ev)
                 eng.iter_global()
 
     iterate(args.warmup)
@@ -488,7 +567,7 @@ def main():
         # eager pass of the same kernels right after the timed graph replay (and, at
         # N > 1, where events inside the timed region would cost ~15 % of a shard's step)
         eng.timing(True)
-        iterate(args.steps)
+        iterate(args.steps, record=multi)
         tm = eng.timing_read()
         timing = "HIP events on an eager pass of the same kernels right after the timed graph replay"
     else:
@@ -500,10 +579,24 @@ def main():
     cand["list_rebuilds"] = st.get("list_rebuilds")
     cand["iterations"] = st["iter"]
     info = eng.layout_info()
+    torch.cuda.synchronize()
+    allreduce_ms = (sum(a.elapsed_time(b) for a, b in ar_events) / len(ar_events)) if ar_events else None
+    per_rank = None
     if world > 1:
-        t = torch.tensor([dt, tm["assign_ms"]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, assign_ms = float(t[0]), float(t[1])
+        # per-rank breakdown of one iteration (eager event pass): assign, update, lists, the
+        # all-reduce (its events include waiting for the slowest rank), the slab size
+        mine = torch.tensor([dt, tm["assign_ms"], tm["tail_ms"], tm.get("candidates_ms", 0.0),
+                             allreduce_ms if allreduce_ms is not None else -1.0, float(eng.n)],
+                            dtype=torch.float64, device="cuda")
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        every = torch.stack(every).cpu().numpy()
+        dt, assign_ms = float(every[:, 0].max()), float(every[:, 1].max())
+        per_rank = {"assign": every[:, 1].round(5).tolist(), "update": every[:, 2].round(5).tolist(),
+                    "tile_lists": every[:, 3].round(5).tolist(),
+                    "allreduce": every[:, 4].round(5).tolist() if allreduce_ms is not None else None,
+                    "points": every[:, 5].astype(np.int64).tolist(),
+                    "wall_ms_per_step": (every[:, 0] * 1e3 / args.steps).round(5).tolist()}
     else:
         assign_ms = tm["assign_ms"]
     launch_ms, b2b_ms = assign_ms, None
@@ -591,9 +684,12 @@ def main():
                          "stream_bytes_per_launch": stream_bytes, "compressed_points": sb["compressed_points"],
                          "stream_GBps": stream_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0,
                          "avg_launch_ms": launch_ms, "avg_launch_ms_back_to_back": b2b_ms,
-                         "timing": timing + ("" if world == 1 else " (max over ranks)")},
+                         "timing": timing + ("" if world == 1 else " (max over ranks)"),
+                         "compute": compute_roofline(n_local, K, D, cand.get("mean", 0.0), launch_ms)},
             "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"],
-                                      "tile_lists": tm.get("candidates_ms", 0.0)},
+                                      "tile_lists": tm.get("candidates_ms", 0.0),
+                                      **({"allreduce": allreduce_ms} if allreduce_ms is not None else {}),
+                                      **({"per_rank": per_rank} if per_rank is not None else {})},
             "candidates": cand,
             "layout_ms": layout_ms,
             "reserve_ms": reserve_ms,   # engine setup (Engine.reserve), before the timed layout
@@ -611,7 +707,20 @@ def main():
         if kpp_ms is not None:
             out["kmeanspp_ms"] = kpp_ms   # GPU k-means++ seeding of the same cloud (K centres), host prep included
         if not args.no_cpu and world == 1:
-            out["cpu_baseline"] = cpu_baseline(X.float().cpu().numpy(), C0.cpu().numpy())
+            Xh, Ch = X.float().cpu().numpy(), C0.cpu().numpy()
+            if args.config == 2:
+                # the whole 20-iteration fit on the CPU and on the GPU, and their parity
+                out["cpu_baseline"], ref = cpu_fit_baseline(Xh, Ch, args.steps)
+                res = pcm_amd.lloyd_fit(X, C0, max_iter=args.steps, tol=0.0)
+                torch.cuda.synchronize()
+                out["parity_vs_cpu"] = {
+                    "labels_bitwise": bool(np.array_equal(res.labels.cpu().numpy(), ref["labels"])),
+                    "centres_bitwise": bool(np.array_equal(res.centers.cpu().numpy(), ref["centers"])),
+                    "n_iter": [int(res.n_iter), int(ref["n_iter"])],
+                    "inertia_equal": float(res.inertia) == ref["inertia"]}
+            else:
+                out["cpu_baseline"] = cpu_baseline(Xh, Ch)
+            out["cpu_numpy"] = numpy_baseline(Xh, Ch)
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -181,6 +181,11 @@ int pcm_candidate_stats(pcm_engine *e, double *mean, int *max, int64_t *full_cel
  * length (synchronising). */
 int pcm_tile_list_stats(pcm_engine *e, int *zlev, int64_t *crowded_tiles, int64_t *listed_tiles, int64_t *listed_len,
                         void *stream);
+/* Crowded layouts, the long-list paths of the assign kernel: tile lists longer
+ * than 256 (scanned through LDS chunks), all-K tiles (a FULL cell's tile with no
+ * list of at most 1024) and the longest tile list (synchronising; 0 when not
+ * crowded). */
+int pcm_tile_list_detail(pcm_engine *e, int64_t *long_lists, int64_t *allk_tiles, int64_t *max_len, void *stream);
 
 /* Kernel timing on the engine's launch stream (HIP events around every launch
  * of the assign kernel and of the candidate and tail kernels).  enable=1 starts

@@ -95,3 +95,41 @@ def test_crowded_2d_and_f16(pcm, monkeypatch):
         ref = R.lloyd_fit(X, C0, max_iter=10, tol=0.0, fast=True)
         np.testing.assert_array_equal(res.labels.cpu().numpy(), ref["labels"])
         np.testing.assert_array_equal(res.centers.cpu().numpy(), ref["centers"])
+
+
+@pytest.mark.parametrize("name,zlev,k,expect", [
+    ("many", "auto", 4096, "long"),       # tile lists of 257..1024 entries: LDS chunks, carried bd/bj
+    ("many", "auto", 1024, "long"),
+    ("clusters", "1", 4096, "allk"),      # one Morton level: a tile spans its whole cluster -> > 1024 -> all K
+    ("clusters", "1", 1024, "long"),
+])
+def test_crowded_long_lists_and_allk_tiles(pcm, name, zlev, k, expect, monkeypatch):
+    """the chunked crowded path of k_lloyd1 (tile lists longer than TLCAP = 256,
+    all-K tiles staged through LDS in 256-centre chunks with the best distance carried
+    across chunks, the direct-mapped LDS table whose j mod 256 collisions spill to global
+    atomics) at K = 1024 and 4096, bitwise against the oracle; candidate_stats must show
+    that the path ran."""
+    X = _cloud(name)
+    n = X.shape[0]
+    C0 = X[R.init_indices(n, k)]
+    if zlev == "auto":
+        monkeypatch.delenv("PCM_ZLEV", raising=False)
+    else:
+        monkeypatch.setenv("PCM_ZLEV", zlev)
+    from pcm_amd.engine import Engine
+    from pcm_amd import lloyd
+    eng = Engine(3, k, torch.float32, max_iter=8)
+    Xt = torch.from_numpy(X).cuda()
+    lloyd.prepare(eng, Xt, lloyd.LOCAL)
+    res = pcm.lloyd_fit(Xt, torch.from_numpy(C0).cuda(), max_iter=8, tol=0.0, engine=eng)
+    torch.cuda.synchronize()
+    st = eng.candidate_stats()
+    print(name, zlev, k, st)
+    if expect == "long":
+        assert st["long_tile_lists"] > 0 and st["tile_list_max"] > 256, st
+    else:
+        assert st["allk_tiles"] > 0, st
+    ref = R.lloyd_fit(X, C0, max_iter=8, tol=0.0, fast=True)
+    np.testing.assert_array_equal(res.labels.cpu().numpy(), ref["labels"])
+    np.testing.assert_array_equal(res.centers.cpu().numpy(), ref["centers"])
+    assert res.n_iter == ref["n_iter"] and res.inertia == ref["inertia"]

@@ -10,14 +10,17 @@ into spatial slabs (histogram all-reduce, stable partition, ``all_to_all`` of
 the points and their global rows), every iteration all-reduces the integer
 statistics, and the final labels travel back to the row owners.
 
-* config 4: N=100M, K=1024, D=3 fp32, 12.5M rows per rank, 2 iterations;
+* config 4: N=100M, K=1024, D=3 fp32, 12.5M rows per rank, 8 iterations (list
+  rebuilds and refreshes on the 12.5M slabs, round 5);
 * config 5: N=500M, K=4096, D=4 fp16, 62.5M rows per rank, 1 iteration (+ the
   final E-step) -- the 4 GB all_to_all, the slab cut and the label return at
   the driver's sizes;
 * config 3: N=100M, K=1024, one GPU, 25 iterations (a bench-length fit through
-  list rebuilds/refreshes on the compressed stream), then EVERY label against
-  the GPU brute-force operator (``pcm_assign_bruteforce``: all K centres, no
-  pruning) and the exact statistics of those labels against the operator's.
+  list rebuilds/refreshes on the compressed stream) bitwise against the C oracle's
+  25-iteration fit (round 5: the whole headline trajectory, not 2 iterations),
+  plus EVERY label against the GPU brute-force operator (``pcm_assign_bruteforce``:
+  all K centres, no pruning) and the exact statistics of those labels against the
+  operator's.
 
 Bar for configs 4/5: labels bit-exact against the C oracle
 (oracle/lloyd_ref.c, OpenMP on the box's host cores, run while the ranks
@@ -125,7 +128,7 @@ def gpu():
 @pytest.mark.timeout(400)
 def test_config4_100m_k1024_8_ranks(gpu):
     n = 100_000_000
-    parts, labels, ref = _run_config(n, 1024, 3, False, 2)
+    parts, labels, ref = _run_config(n, 1024, 3, False, 8)
     _compare(parts, labels, ref, n)
 
 
@@ -136,12 +139,13 @@ def test_config5_500m_k4096_d4_fp16_8_ranks(gpu):
     _compare(parts, labels, ref, n)
 
 
-@pytest.mark.timeout(300)
-def test_config3_bench_length_fit_matches_bruteforce(gpu):
-    """25 iterations at N=100M (the bench's warm-up + timed steps), then all
-    100M final labels against the brute-force operator at the final centres,
-    and the exact integer statistics of the engine's labels against the
-    operator's own accumulation."""
+@pytest.mark.timeout(400)
+def test_config3_bench_length_fit_matches_oracle(gpu):
+    """25 iterations at N=100M (the bench's warm-up + timed steps) bitwise against
+    oracle/lloyd_ref.c's 25-iteration fit of the same cloud (labels, centres,
+    n_iter, change records, exact inertia); then all 100M final labels against the
+    brute-force operator at the final centres, and the exact integer statistics of
+    the engine's labels against the operator's own accumulation."""
     import pcm_amd
     from pcm_amd.engine import assign_bruteforce, synth_rows, synth_uniform
     from pcm_amd.fixed import fixed_q
@@ -151,6 +155,16 @@ def test_config3_bench_length_fit_matches_bruteforce(gpu):
     res = pcm_amd.lloyd_fit(X, C0, max_iter=iters, tol=0.0)
     torch.cuda.synchronize()
     assert res.n_iter == iters and res.layout["ntiles"] > 0
+    # the whole trajectory against the oracle (sklearn _kmeans_single_lloyd, _kmeans.py:623-752)
+    Xh = X.cpu().numpy()
+    ref = R.lloyd_fit(Xh, Xh[R.init_indices(n, k)].copy(), max_iter=iters, tol=0.0, fast=True)
+    del Xh
+    assert res.n_iter == ref["n_iter"]
+    bad = np.flatnonzero(res.labels.cpu().numpy() != ref["labels"])
+    assert bad.size == 0, f"{bad.size} labels differ from the oracle, first rows {bad[:8]}"
+    assert np.array_equal(res.centers.cpu().numpy(), ref["centers"])
+    np.testing.assert_array_equal(np.asarray(res.changed) > 0, np.asarray(ref["changed"], np.int64) > 0)
+    assert float(res.inertia) == ref["inertia"]
     q = fixed_q(X.abs().amax(0).double().cpu().numpy())
     stats = torch.zeros(k * (d + 1), dtype=torch.int64, device="cuda")
     lab_bf = assign_bruteforce(X, res.centers, q, stats)
