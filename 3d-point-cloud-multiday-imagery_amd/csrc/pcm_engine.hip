@@ -58,6 +58,8 @@ struct pcm_engine {
     long long ntiles = 0;            // host copy: -1 = not read back yet (pcm_layout_info reads it)
     long long ntiles_cap = 0;        // upper bound on the tiles of the current layout (grid sizing)
     uint32_t tile_cap = TILE;        // points per tile
+    uint32_t tile_cap_big = TILE_BIG;   // ... in cells single-signed on every axis (cell_tile_cap)
+    uint32_t *ntiles_host = nullptr; // pinned: the layout's tile count, read back at the end of pcm_layout_build
     // device buffers (persistent: grown on demand, reused by later layouts, freed at destroy)
     void *xs = nullptr;
     unsigned *xz = nullptr;          // compressed 8-B point records (fp32 D = 3, k_tile_compress)
@@ -342,6 +344,21 @@ void make_grid(Grid &g, int d, const double *lo, const double *hi, double target
     g.prune = (maxext < 1e18) ? 1 : 0;
 }
 
+// Assign blocks (the fine-grid k_lloyd1 instance: 8 lane slots, no masks) the
+// chip holds at once, from the occupancy API.
+int lloyd1_resident(const pcm_engine *e) {
+    int per_cu = 0;
+    const int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
+        using TT = decltype(T);
+        constexpr int D = decltype(DD)::value;
+        const size_t lds = (size_t)AccL<D, 8>::words * sizeof(uint32_t);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_lloyd1<TT, D, 8, false>, TPB,
+                                                            lds) == hipSuccess ? 0 : 1;
+    });
+    if (rc || per_cu < 1) return 0;
+    return per_cu * e->num_cu;
+}
+
 // The Lloyd engine's pruning grid: about min(32 K, n / 2800) cells -- ~2.8k
 // points per cell: fewer, fuller tiles (a tile round is 1024 points) outweigh
 // the slightly longer candidate lists (swept on 12.5M / 100M clouds).
@@ -355,8 +372,26 @@ void choose_grid(pcm_engine *e) {
     const double share = e->n_global > 0 ? std::min(1.0, (double)e->n / (double)e->n_global) : 1.0;
     const double per_centre = e->d >= 4 ? 48.0 : 32.0;
     double target = std::min(per_centre * e->k * share, (double)e->n / (e->d >= 4 ? 1000.0 : 2800.0));
+    // One generation (round 5): when the cells would outnumber the assign blocks
+    // the chip holds at once but the cloud fits that many tiles of <= ~0.6 TILE_BIG
+    // points (an 8-way config-4 slab: 12.5M points, 4096 cells = ~1.4 generations,
+    // whose second one costs a whole block lifetime), take fewer, fuller cells so
+    // that every tile's block starts at once.
+    const double fill = [] { const char *v = std::getenv("PCM_ONEGEN_FILL"); return v ? std::atof(v) : 0.85; }();
+    const double resident = fill * (double)lloyd1_resident(e);
+    bool onegen = false;
+    if (e->d <= 3 && fill > 0.0 && e->tile_cap_big > e->tile_cap && resident >= 1.0 && target > resident &&
+        (double)e->n <= 0.6 * TILE_BIG * resident) {
+        target = resident;
+        onegen = true;
+    }
     if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     make_grid(e->g, e->d, e->lo, e->hi, target);
+    // make_grid rounds each axis: shrink the target until the cells fit the generation
+    for (int it = 0; onegen && it < 16 && (double)e->g.ncells > resident; ++it) {
+        target *= 0.95;
+        make_grid(e->g, e->d, e->lo, e->hi, target);
+    }
     if (e->k <= 1) e->g.prune = 0;
 }
 
@@ -434,6 +469,7 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->empty_idx, (size_t)k * sizeof(int));
     err = err ? err : hipMalloc(&e->ntiles_dev, 2 * sizeof(uint32_t));
     err = err ? err : hipMalloc(&e->zpts, 32 * 16 * sizeof(unsigned long long));
+    err = err ? err : hipHostMalloc((void **)&e->ntiles_host, sizeof(uint32_t), hipHostMallocDefault);
     err = err ? err : hipMemset(e->partials, 0, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMemset(e->ctrl, 0, sizeof(Ctrl));
     if (err != hipSuccess) {
@@ -459,6 +495,7 @@ int pcm_engine_destroy(pcm_engine *e) {
                   e->grows, e->zpts};
     for (void *p : ps)
         if (p) (void)hipFree(p);
+    if (e->ntiles_host) (void)hipHostFree(e->ntiles_host);
     delete e;
     return 0;
 }
@@ -629,6 +666,9 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     // the assign kernel addresses points with 32-bit offsets and uses offset
     // 0x0ffffff0 (points) as its always-out-of-range prefetch
     if (e->npad >= 0x0ffffff0LL) return fail(PCM_E_ARG, "at most 2^28 - 32 points per engine (shard larger clouds)");
+    // points per tile of single-signed cells (PCM_TILE_BIG=0 keeps TILE everywhere: A/B only)
+    static const bool big_on = [] { const char *v = std::getenv("PCM_TILE_BIG"); return !(v && std::atoi(v) == 0); }();
+    e->tile_cap_big = big_on ? (uint32_t)TILE_BIG : (uint32_t)TILE;
     choose_grid(e);
     const long long nc = e->g.ncells;
     const size_t ts = tsize(e->dtype);
@@ -639,7 +679,9 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         return (uint32_t)std::min(TILE, std::max(4 * TPB, c));
     }();
     e->tile_cap = tcap;
-    // every cell holds ceil(count / cap) <= count / cap + 1 tiles
+    if (tcap < (uint32_t)TILE) e->tile_cap_big = tcap;
+    // every cell holds ceil(count / cap) <= count / cap + 1 tiles (single-signed
+    // cells fewer: up to TILE_BIG points each)
     e->ntiles_cap = nc + n / e->tile_cap + 1;
     e->ntiles = -1;
 
@@ -732,15 +774,31 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, sh, e->cell_start);
         LAUNCHCHK();
     }
-    k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap);
+    if (int rc2 = dispatch_d(e->d, [&](auto DD) -> int {
+            constexpr int D = decltype(DD)::value;
+            k_tile_counts<D><<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap, e->tile_cap_big, e->g);
+            LAUNCHCHK();
+            return 0;
+        }))
+        return rc2;
     LAUNCHCHK();
     size_t sb = scan_bytes;
     if (rocprim::exclusive_scan(tmp, sb, tcnt, e->tile_off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s) != hipSuccess)
         return fail(PCM_E_HIP, "layout: tile scan");
     k_tile_total<<<1, 64, 0, s>>>(e->tile_off, tcnt, nc, e->ntiles_dev);
     LAUNCHCHK();
-    k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles, e->tile_cap);
-    LAUNCHCHK();
+    if (int rc2 = dispatch_d(e->d, [&](auto DD) -> int {
+            constexpr int D = decltype(DD)::value;
+            k_tile_write<D><<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles, e->tile_cap,
+                                                           e->tile_cap_big, e->g);
+            LAUNCHCHK();
+            return 0;
+        }))
+        return rc2;
+    // the exact tile count for the grids of the per-tile kernels (the bound
+    // ntiles_cap launched ~1.7x as many blocks at config 3, the excess exiting
+    // after one memory latency: a drain tail on every assign launch)
+    HIPCHK(hipMemcpyAsync(e->ntiles_host, e->ntiles_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     // compressed point stream for k_lloyd1 (fp32, D = 3; PCM_XZ=0 disables it: A/B measurement only)
     static const bool xz_on = [] { const char *v = std::getenv("PCM_XZ"); return !(v && std::atoi(v) == 0); }();
     e->use_xz = xz_on && e->dtype == PCM_F32 && e->d == 3;
@@ -748,7 +806,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     if (e->use_xz) {
         HIPCHK(ensure(e->xz, e->cap_xz, (size_t)align_up(e->npad) * 8));   // whole 256-point blocks (zword)
         HIPCHK(ensure(e->tmeta, e->cap_tmeta, (size_t)e->ntiles_cap * sizeof(uint4)));
-        k_tile_compress<<<(int)e->ntiles_cap, 256, 0, s>>>((const float *)e->xs, e->tiles, e->ntiles_dev, e->tmeta,
+        k_tile_compress<<<(int)std::max(1LL, e->ntiles_cap), 256, 0, s>>>((const float *)e->xs, e->tiles, e->ntiles_dev, e->tmeta,
                                                            e->xz, e->zpts);
         LAUNCHCHK();
     }
@@ -766,9 +824,11 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         });
         if (rc) return rc;
     }
-    // stream-ordered: no host synchronisation (work queued later on `stream`
-    // sees the layout; X must not be modified by other streams meanwhile),
-    // except choose_zlev's occupancy read-back
+    // one host synchronisation at the end (the tile count; and choose_zlev's
+    // occupancy read-back): X must not be modified by other streams meanwhile
+    HIPCHK(hipStreamSynchronize(s));
+    e->ntiles = (long long)*e->ntiles_host;
+    if (e->ntiles > e->ntiles_cap) return fail(PCM_E_HIP, "layout: tile count exceeds its bound");
     e->layout_ready = true;
     return 0;
 }
@@ -844,6 +904,14 @@ static int ensure_coarse(pcm_engine *e) {
     return 0;
 }
 
+// k_lloyd1 and the per-tile kernels: one block per tile of the layout (the
+// exact count, read back at layout time).  Measured at config 3: 211 us per
+// launch with one tile per block vs 238 us for as many persistent blocks as are
+// co-resident walking tiles b, b + G, ... (each tile's list install stalled its
+// block; with one tile per block the other resident blocks keep streaming);
+// config-5 shape 485 vs 536 us.
+static int lloyd_grid(const pcm_engine *e) { return (int)std::max(1LL, e->ntiles >= 0 ? e->ntiles : e->ntiles_cap); }
+
 static int launch_candidates(pcm_engine *e, hipStream_t s, int gate) {
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
@@ -873,7 +941,7 @@ static int launch_tile_lists(pcm_engine *e, hipStream_t s, int gate) {
     if (e->zlev <= 0 || e->n == 0) return 0;
     return dispatch_d(e->d, [&](auto DD) -> int {
         constexpr int D = decltype(DD)::value;
-        k_tile_cand<D><<<(int)e->ntiles_cap, 256, 0, s>>>(e->tiles, e->ntiles_dev, e->fc_cnt, e->tbox, e->C, e->k,
+        k_tile_cand<D><<<lloyd_grid(e), 256, 0, s>>>(e->tiles, e->ntiles_dev, e->fc_cnt, e->tbox, e->C, e->k,
                                                           e->tl_cnt, e->tl_rec, e->tl_lab, e->ctrl, gate);
         LAUNCHCHK();
         return 0;
@@ -887,16 +955,8 @@ static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, TPB, lds) != hipSuccess || per_cu < 1)
         per_cu = 2;
     if (const char *ov = std::getenv("PCM_ASSIGN_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(ov));
-    return (int)std::max(1LL, std::min<long long>(e->ntiles_cap, (long long)per_cu * e->num_cu));
+    return (int)std::max(1LL, std::min<long long>(e->ntiles >= 0 ? e->ntiles : e->ntiles_cap, (long long)per_cu * e->num_cu));
 }
-
-// k_lloyd1: one block per tile (the grid covers the layout's tile bound; blocks
-// past the device tile count exit at once).  Measured at config 3: 211 us per
-// launch for k_lloyd with one tile per block vs 238 us for as many persistent
-// blocks as are co-resident walking tiles b, b + G, ... (each tile's list
-// install stalled its block; with one tile per block the other resident blocks
-// keep streaming); config-5 shape 485 vs 536 us.
-static int lloyd_grid(const pcm_engine *e) { return (int)std::max(1LL, e->ntiles_cap); }
 
 static int lloyd_slots(const pcm_engine *e) {
     if (const char *ov = std::getenv("PCM_LSLOT_RT")) return std::atoi(ov) == 8 ? 8 : LSLOT;   // tuning sweeps only
@@ -1028,10 +1088,7 @@ static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
                 // crowded layouts: + the long tile lists' int64 words (AccL::gwords)
                 const size_t lds = e->zlev > 0 ? AccL<D, LS>::bytes_crowded
                                                 : (size_t)AccL<D, LS>::words * sizeof(uint32_t);
-                if (std::getenv("PCM_ASSIGN_BLOCKS_PER_CU"))   // persistent tile walk (tuning sweeps only)
-                    k_lloyd<TT, D, LS><<<assign_grid(e, (const void *)k_lloyd<TT, D, LS>, lds), TPB, lds, s>>>(
-                        A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt);
-                else if (e->zlev > 0)   // crowded layout (sub-cell masks off: e->sub = 0)
+                if (e->zlev > 0)   // crowded layout (sub-cell masks off: e->sub = 0)
                     k_lloyd1<TT, D, LS, false, true><<<lloyd_grid(e), TPB, lds, s>>>(
                         A, e->tiles, e->fc_rec, e->fc_lab, e->C, e->fc_cnt, e->tl_rec);
                 else

@@ -2,7 +2,7 @@
 //
 // Hot path: per iteration
 //   k_cand             exact candidate lists per grid cell (fp64 bisector bound)
-//   k_lloyd            nearest centroid over the cell's candidates + LDS-privatised
+//   k_lloyd1           nearest centroid over the cell's candidates + LDS-privatised
 //                      fixed-point accumulation (replaces _k_means_lloyd.pyx:168-218)
 //   k_label            final E-step: labels + inertia (_kmeans.py:736-750)
 //   k_global           averaging / shift / convergence (_k_means_common.pyx:274-311,
@@ -29,6 +29,12 @@ constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-
 #endif
 constexpr int TPB = PCM_TPB;       // assign block size
 constexpr int TILE = 32 * TPB;     // max points per tile: <= 32 per lane, 64 per shared LDS word (see AccL)
+// Tiles of cells that are single-signed on every axis may hold up to TILE_BIG
+// points (round 5): a shared LDS word then sums <= 128 values of one known sign,
+// |sum| < 2^32, recovered exactly from the word read as unsigned (k_lloyd1's
+// fold, cell_signs).  Fewer, fuller tiles let a small slab's launch fit in one
+// generation of resident blocks (choose_grid).
+constexpr int TILE_BIG = 64 * TPB;
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int TLCAP = 256;        // tile lists staged whole in k_lloyd1's LDS (slot-map path)
 constexpr int TLMAX = 1024;       // tile-list capacity (longer lists: FULL); lists past TLCAP scan in LDS chunks
@@ -312,12 +318,46 @@ __device__ __forceinline__ long long xs_index(long long i, int a) {
     return ((i >> 2) * D + a) * 4 + (i & 3);
 }
 
+// Sign of every axis over a cell: 2 bits per axis, 1 = every point binned there
+// is >= 0 (the cell box's lower edge, binning fuzz included, is >= 0), 2 = every
+// point <= 0, 0 = the cell may hold both signs.  -0.0 counts as either: its
+// fixed-point value is 0.
+template <int D>
+__device__ __forceinline__ unsigned cell_signs(const Grid &g, unsigned cell) {
+    int ci[MAXD];
+    for (int a = D - 1, c = (int)cell; a >= 0; --a) {   // cell ids fit 32 bits (sort keys)
+        ci[a] = (int)((unsigned)c % (unsigned)g.G[a]);
+        c = (int)((unsigned)c / (unsigned)g.G[a]);
+    }
+    double blo[MAXD], bhi[MAXD];
+    cell_box<D>(g, ci, ci, blo, bhi);
+    unsigned m = 0u;
+#pragma unroll
+    for (int a = 0; a < D; ++a) m |= (blo[a] >= 0.0 ? 1u : (bhi[a] <= 0.0 ? 2u : 0u)) << (2 * a);
+    return m;
+}
+template <int D>
+__device__ __forceinline__ bool cell_single_signed(unsigned m) {
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < D; ++a) ok = ok && ((m >> (2 * a)) & 3u) != 0u;
+    return ok;
+}
+// points per tile of cell c: capbig when the cell is single-signed on every axis
+template <int D>
+__device__ __forceinline__ uint32_t cell_tile_cap(const Grid &g, unsigned c, uint32_t cap, uint32_t capbig) {
+    return (capbig > cap && cell_single_signed<D>(cell_signs<D>(g, c))) ? capbig : cap;
+}
+
+template <int D>
 __global__ __launch_bounds__(256) void k_tile_counts(const uint32_t *__restrict__ start, long long ncells,
-                                                     uint32_t *__restrict__ cnt, uint32_t cap) {
+                                                     uint32_t *__restrict__ cnt, uint32_t cap, uint32_t capbig,
+                                                     Grid g) {
     long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (c >= ncells) return;
-    uint32_t n = start[c + 1] - start[c];
-    cnt[c] = (n + cap - 1) / cap;
+    const uint32_t n = start[c + 1] - start[c];
+    const uint32_t cp = cell_tile_cap<D>(g, (unsigned)c, cap, capbig);
+    cnt[c] = (n + cp - 1) / cp;
 }
 
 // tile_off[nc] and the tile count (the scan is exclusive: add the last cell's count)
@@ -329,14 +369,17 @@ __global__ void k_tile_total(uint32_t *__restrict__ off, const uint32_t *__restr
     *ntiles = t;
 }
 
+template <int D>
 __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__ start, const uint32_t *__restrict__ off,
-                                                    long long ncells, uint4 *__restrict__ tiles, uint32_t cap) {
+                                                    long long ncells, uint4 *__restrict__ tiles, uint32_t cap,
+                                                    uint32_t capbig, Grid g) {
     long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (c >= ncells) return;
     uint32_t s = start[c], e = start[c + 1];
     uint32_t n = e - s;
     if (n == 0) return;
-    uint32_t nt = (n + cap - 1) / cap;
+    const uint32_t cp = cell_tile_cap<D>(g, (unsigned)c, cap, capbig);
+    uint32_t nt = (n + cp - 1) / cp;
     uint32_t per = (n + nt - 1) / nt;
     uint32_t o = off[c];
     for (uint32_t t = 0; t < nt; ++t) {
@@ -388,17 +431,16 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
     const uint4 tr = tiles[t];
     const unsigned start = tr.y, end = tr.z;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    // the whole tile (<= TILE = 16 x 256 points) in registers: every load in
+    // the whole tile (<= TILE_BIG = 32 x 256 points) in registers: every load in
     // flight at once, one read of xs (a strided loop waited one latency per
     // round, twice: 505-530 us for 100M points)
-    constexpr int PPT = TILE / 256;
+    constexpr int PPT = TILE_BIG / 256;
     unsigned bits[PPT][3];
 #pragma unroll
     for (int u = 0; u < PPT; ++u) {
         const unsigned i = start + tid + 256u * u;
-        const unsigned ii = i < end ? i : start;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) bits[u][a] = __float_as_uint(xs[xs_index<3>(ii, a)]);
+        for (int a = 0; a < 3; ++a) bits[u][a] = i < end ? __float_as_uint(xs[xs_index<3>(i, a)]) : 0u;
     }
     unsigned mn[3] = {~0u, ~0u, ~0u}, mx[3] = {0u, 0u, 0u}, sor[3] = {0u, 0u, 0u}, sand[3] = {1u, 1u, 1u};
 #pragma unroll
@@ -1437,7 +1479,7 @@ __global__ void k_inert_fold(unsigned long long *__restrict__ rep, unsigned long
 
 // E-step with the current centres writing labels (sorted order) and the
 // inertia (final E-step of _kmeans.py:736-750, relocation keys).  Not gated.
-// Same tile walk and candidate lists as k_lloyd; 4 points per lane per round,
+// Same tiles and candidate lists as k_lloyd1 (persistent blocks); 4 points per lane per round,
 // the loads of the next round in flight while one is computed; compressed
 // tiles read their 8-B records (round 4), like k_lloyd1.
 template <typename T, int D, typename LT>
@@ -1534,20 +1576,12 @@ __global__ __launch_bounds__(TPB) void k_label(LloydArgs A, void *lab, unsigned 
 // shift 0 <= tol, so sklearn stops at that same iteration either way (DESIGN.md
 // "Convergence").
 //
-// Per tile (cell): the candidate list (ascending centroid index, so the
-// strict-'<' scan keeps the lowest index on ties, _k_means_lloyd.pyx:205-213)
-// in LDS; a winner at list position j < LSLOT is summed into the thread's
-// LDS words of slot j (ds_add_u32, lane-minor: conflict-free);
-// positions >= LSLOT (lists longer than LSLOT) use global int64 atomics.
-// Out-of-tile lanes of a partial round add into a junk slot (never read).
-// Persistent blocks walk tiles blockIdx.x, +gridDim.x, ...; the loads of the
-// next two work items (1024 points each) are in flight while one is computed.
-//
-// The point loads are the ONLY vector-memory loads of the loop: tile headers,
-// candidate lists and the all-centre scan of FULL tiles use scalar (SMEM)
-// loads.  A vector load whose result is consumed a tile later makes the
-// compiler's waitcnt analysis fall back to vmcnt(0) at every work item, which
-// collapses the two-item prefetch (measured: 2x the kernel time).
+// Per tile (a run of one cell's points): the candidate list (ascending centroid
+// index, so the strict-'<' scan keeps the lowest index on ties,
+// _k_means_lloyd.pyx:205-213) in LDS; a winner's fixed-point coordinates and
+// count are summed into LDS words of its lane slot (ds_add_u32, lane-minor:
+// conflict-free), winners without a slot into int64 words; out-of-tile lanes of
+// a partial round add into a junk slot (never read).
 // Nearest of mm centres read through scalar loads (FULL tiles: the whole
 // uniform centre array); same scan order and tie rule as scan4.
 template <int D>
@@ -1571,228 +1605,9 @@ __device__ __forceinline__ void scan4_s(const float4 *__restrict__ C, int mm, co
 #ifndef PCM_WPE
 #define PCM_WPE 4
 #endif
-template <typename T, int D, int LS>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(PCM_WPE, 8))) void k_lloyd(LloydArgs A, const uint4 *__restrict__ tiles,
-                                               const float4 *__restrict__ fc_rec,
-                                               const int32_t *__restrict__ fc_lab,
-                                               const float4 *__restrict__ Call,
-                                               const uint32_t *__restrict__ fc_cnt) {
-    if (gated(A.ctrl)) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LS+1)*(D+1)][TPB]
-    __shared__ float4 crec[2][CAPF];
-    __shared__ int32_t cid[2][CAPF];
-    // list positions LS .. CAPF-1 of long (non-FULL) lists: block-shared int64
-    // words (ds_add_u64), folded at the tile boundary like the slots.  Used by
-    // the 8-slot variant (fine grids, short lists: the smaller LDS footprint
-    // gives 5 waves/SIMD) and at D = 4 (long lists are the norm there); the
-    // 16-slot D <= 3 variant leaves them out (1.5 KB would cost a resident
-    // block per CU) and sends the rare long list to global int64 atomics.
-    constexpr bool kOvf = D >= 4 || LS <= 8;   // 8 slots: LDS int64 words past them; 12 / 16: global atomics (rare positions)
-    __shared__ unsigned long long ovf[kOvf ? (CAPF - LS) * (D + 1) : 1];
-    const int tid = threadIdx.x;
-    const unsigned G = gridDim.x;
-    const unsigned nt = *A.ntiles;
-    unsigned t = blockIdx.x;
-    if (t >= nt) return;
-    DBG_L(0);
-    const float4 *lrec = fc_rec;
-    const int32_t *llab = fc_lab;
-    // tile record with .w := the cell's candidate count (dependent scalar load)
-    auto tile_at = [&](unsigned i) {
-        uint4 v = tiles[i < nt ? i : nt - 1];
-        v.w = fc_cnt[v.x];
-        return v;
-    };
-    const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
-    for (int e = tid; e < AccL<D, LS>::words; e += TPB) acc[e] = 0u;
-    if (kOvf)
-        for (int e = tid; e < (CAPF - LS) * (D + 1); e += TPB) ovf[e] = 0ull;
-    uint32_t *const myacc = acc + (tid & (AW - 1));
-
-    // Candidate list of tile hh into LDS half sp: scalar loads, 4 records per
-    // chunk, written by lanes 0-3 (uniform cell -> SMEM, no vector loads).
-    auto install = [&](const TileL &hh, int sp) {
-        if (hh.full) {
-            if (tid < LS) cid[sp][tid] = tid;
-            return;
-        }
-        const float4 *pr = lrec + (size_t)hh.cell * CAPF;
-        const int4 *pl = reinterpret_cast<const int4 *>(llab + (size_t)hh.cell * CAPF);
-        for (int j0 = 0; j0 < hh.mm; j0 += 4) {
-            const float4 v0 = pr[j0], v1 = pr[j0 + 1], v2 = pr[j0 + 2], v3 = pr[j0 + 3];
-            const int4 ids = pl[j0 >> 2];
-            if (tid < 4) {
-                const float4 v = tid == 0 ? v0 : tid == 1 ? v1 : tid == 2 ? v2 : v3;
-                const int id = tid == 0 ? ids.x : tid == 1 ? ids.y : tid == 2 ? ids.z : ids.w;
-                crec[sp][j0 + tid] = v;
-                cid[sp][j0 + tid] = id;
-            }
-        }
-    };
-    TileL h = make_tile(tile_at(t), A.K);
-    install(h, 0);
-    TileL h1 = make_tile(tile_at(t + G), A.K);
-    TileL h2 = make_tile(tile_at(t + 2 * G), A.K);
-    uint4 tl3 = tile_at(t + 3 * G);
-
-    int r = 0;
-    // Lanes past their tile's end get the out-of-range offset: the buffer load
-    // returns zeros without touching memory (no re-read of the next cell's rows).
-    auto item_off = [&](int k) -> unsigned {
-        int rr = r + k;
-        unsigned o, e;
-        if (rr < h.nr) {
-            o = h.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
-            e = h.end;
-        } else {
-            rr -= h.nr;
-            if (t + G >= nt) return 0x0ffffff0u;
-            if (rr < h1.nr) {
-                o = h1.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
-                e = h1.end;
-            } else {
-                rr -= h1.nr;
-                if (t + 2 * G >= nt) return 0x0ffffff0u;
-                o = h2.base0 + (unsigned)rr * 4u * TPB + 4u * tid;
-                e = h2.end;
-            }
-        }
-        return o < e ? o : 0x0ffffff0u;
-    };
-
-    Raw<T, D> xa, xb, xc;
-    LOAD_X(xa, item_off(0));
-    LOAD_X(xb, item_off(1));
-    __syncthreads();
-    DBG_L(1);
-
-    unsigned long long *prep = A.partials + (size_t)(A.ctrl->iter & 1u) * A.pstride;
-    int par = 0;
-
-    auto step = [&](Raw<T, D> &cx, Raw<T, D> &nx) -> bool {
-        const bool last_round = (r + 1 == h.nr);
-        LOAD_X(nx, item_off(2));
-        const unsigned rbase = h.base0 + (unsigned)r * 4u * TPB;
-        const unsigned i0 = rbase + 4u * tid;
-        float x[4][D];
-        unpack_x<D>(cx, x);
-        int bj[4];
-        if (h.mm == 1) {
-            for (int e = 0; e < 4; ++e) bj[e] = 0;
-        } else {
-            float bd[4];
-            if (h.full) scan4_s<D>(Call, h.mm, x, bd, bj);
-            else scan4<D>(crec[par], h.mm, x, bd, bj);
-        }
-        // block-uniform: every point of the round lies inside the tile
-        const bool whole = (rbase >= h.start) && (rbase + 4u * TPB <= h.end);
-        int sl[4];
-        bool over = false;
-        for (int e = 0; e < 4; ++e) {
-            const bool v = whole || ((i0 + e >= h.start) && (i0 + e < h.end));
-            const bool hi = bj[e] >= LS;
-            over |= v && hi;
-            sl[e] = (v && !hi) ? bj[e] : LS;
-        }
-        for (int e = 0; e < 4; ++e) {
-            uint32_t *ap = myacc + sl[e] * ((D + 1) * AW);
-            for (int a = 0; a < D; ++a) atomicAdd(ap + a * AW, (uint32_t)fixed_i(x[e][a], A.q[a]));
-            atomicAdd(ap + D * AW, 1u);
-        }
-        if (over) {   // list positions >= LS (long lists only)
-            for (int e = 0; e < 4; ++e) {
-                const bool v = whole || ((i0 + e >= h.start) && (i0 + e < h.end));
-                if (!(v && bj[e] >= LS)) continue;
-                // non-FULL: the block's LDS int64 words; FULL (all K): global int64.
-                // Two branches with one address space each: a pointer select
-                // would make these FLAT atomics, which count in vmcnt AND lgkmcnt
-                // and made the waitcnt pass drain every load (vmcnt(0)) before
-                // each work item's prefetch.
-                if (h.full || !kOvf) {
-                    unsigned long long *pp = prep + (size_t)(h.full ? bj[e] : cid[par][bj[e]]) * (D + 1);
-                    for (int a = 0; a < D; ++a)
-                        atomicAdd(pp + a, (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
-                    atomicAdd(pp + D, 1ull);
-                } else {
-                    const int o = (bj[e] - LS) * (D + 1);
-                    for (int a = 0; a < D; ++a)
-                        atomicAdd(&ovf[o + a], (unsigned long long)(long long)fixed_i(x[e][a], A.q[a]));
-                    atomicAdd(&ovf[o + D], 1ull);
-                }
-            }
-        }
-        if (!last_round) {
-            ++r;
-            return true;
-        }
-        // ---- tile boundary: fold the slot sums of h, install h1's candidates
-        DBG_L(2);
-        __syncthreads();
-        {
-            const int nslots = h.mm < LS ? h.mm : LS;
-            const int npairs = nslots * (D + 1);
-            // 16 threads per (slot, a) row, each summing AW/16 of its words
-            for (int p0 = 0; p0 < npairs; p0 += TPB / 16) {
-                const int pi = p0 + tid / 16, sub = tid & 15;
-                long long sacc = 0;
-                if (pi < npairs) {
-                    const bool cnt = (pi % (D + 1) == D);
-                    uint32_t *row = acc + pi * AW;
-                    for (int k = 0; k < AW / 16; ++k) {
-                        uint32_t *ap = row + sub + 16 * k;
-                        sacc += cnt ? (long long)*ap : (long long)(int32_t)*ap;
-                        *ap = 0u;
-                    }
-                }
-                sacc += __shfl_down(sacc, 8, 16);
-                sacc += __shfl_down(sacc, 4, 16);
-                sacc += __shfl_down(sacc, 2, 16);
-                sacc += __shfl_down(sacc, 1, 16);
-                if (pi < npairs && sub == 0 && sacc) {
-                    const int slot = pi / (D + 1), qq = pi % (D + 1);
-                    atomicAdd(prep + (size_t)cid[par][slot] * (D + 1) + qq, (unsigned long long)sacc);
-                }
-            }
-            if (kOvf && !h.full && h.mm > LS)
-                for (int i = tid; i < (h.mm - LS) * (D + 1); i += TPB) {
-                    const unsigned long long w = ovf[i];
-                    if (w) {
-                        atomicAdd(prep + (size_t)cid[par][LS + i / (D + 1)] * (D + 1) + i % (D + 1), w);
-                        ovf[i] = 0ull;
-                    }
-                }
-        }
-        if (t + G >= nt) {
-            DBG_L(3);
-            // The structurizer routes every step's exit through the loop latch, so
-            // the waitcnt pass merges this path's pending point loads into the
-            // loop header's state and would drain the whole pipeline (vmcnt(0))
-            // before each iteration's first prefetch.  Draining here (the block
-            // is done) keeps the header state that of the third step.
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
-            return false;
-        }
-        install(h1, par ^ 1);
-        par ^= 1;
-        h = h1;
-        h1 = h2;
-        t += G;
-        r = 0;
-        h2 = make_tile(tl3, A.K);
-        tl3 = tile_at(t + 3 * G);
-        __syncthreads();
-        return true;
-    };
-    while (true) {
-        if (!step(xa, xc)) break;
-        if (!step(xb, xa)) break;
-        if (!step(xc, xb)) break;
-    }
-}
-
-// One Lloyd iteration's E-step + accumulation, ONE TILE PER BLOCK (the
-// default launch).  Same arithmetic, slots and fold as k_lloyd; what differs
-// is the block's start-up: the tile record, the candidate count and the first
+// One Lloyd iteration's E-step + accumulation, ONE TILE PER BLOCK (the round-1
+// persistent tile walk, removed in round 5, measured 211 vs 238 us at config 3).
+// The block's start-up: the tile record, the candidate count and the first
 // LSPEC list records (vector loads, speculative: the count is not known yet)
 // and the first two work items' point loads are all issued before anything
 // is waited for, so a block starts scanning one point-load latency after it
@@ -1888,6 +1703,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     for (int o = 0; o <= NSUB; ++o) ss[o] = (MASK && A.sub) ? A.sub_start[((size_t)cell << D) + o] : 0u;
     const unsigned base0 = start & ~3u;
     const int nr = (int)((end - base0 + 4 * TPB - 1) / (4 * TPB));
+    // a tile longer than TILE (<= TILE_BIG: single-signed cells only, k_tile_write)
+    // puts up to 128 values in a shared LDS word: its fold reads coordinate words
+    // by the cell's per-axis sign (cell_signs), else as int32
+    const unsigned sgn = (end - start > (unsigned)TILE) ? cell_signs<D>(A.g, cell) : 0u;
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     // compressed tile (k_tile_compress): 8-B records from xz, decoded exactly
     const bool zc = ZOK && (zm.w >> 31);
@@ -1903,7 +1722,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     };
     __shared__ unsigned long long omask[NSUB];
     __shared__ uint32_t okey[NSUB];
-    __shared__ unsigned long long rmask[16];   // rounds of one tile: <= TILE / (4 TPB) + 1
+    __shared__ unsigned long long rmask[TILE_BIG / (4 * TPB) + 1];   // rounds of one tile
     // The rest of the kernel, instantiated per point format: compressed tiles
     // (fp32 D = 3, 8-B records) issue 2 b128 loads per work item, raw tiles
     // D * sizeof(T) / 4 -- one constant load count per instance keeps hipcc's
@@ -2240,7 +2059,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             }
         }
     };
-    // PF+1 rotating register sets; a tile holds at most TILE / (4 TPB) = 8 rounds
+    // PF+1 rotating register sets; a tile spans at most TILE_BIG / (4 TPB) + 1 = 17 rounds
     for (int r = 0; r < nr; r += PF + 1) {
 #pragma unroll
         for (int k = 0; k <= PF; ++k) step(xr[k], xr[(k + PF) % (PF + 1)], r + k);
@@ -2255,11 +2074,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             const int pi = p0 + tid / 16, sub = tid & 15;
             long long sacc = 0;
             if (pi < npairs) {
-                const bool isc = (pi % (D + 1) == D);
+                const int qa = pi % (D + 1);
+                // word mode: 0 int32 (tiles <= TILE), 1 unsigned (counts; axes >= 0 of a
+                // longer tile), 2 non-positive axis of a longer tile (sum in (-2^32, 0])
+                const unsigned md = (qa == D) ? 1u : ((sgn >> (2 * qa)) & 3u);
                 const uint32_t *row = acc + pi * AW;
                 for (int k = 0; k < AW / 16; ++k) {
                     const uint32_t w = row[sub + 16 * k];
-                    sacc += isc ? (long long)w : (long long)(int32_t)w;
+                    sacc += md == 0u ? (long long)(int32_t)w
+                                     : (md == 1u ? (long long)w : (w ? (long long)w - (1ll << 32) : 0ll));
                 }
             }
             sacc += __shfl_down(sacc, 8, 16);

@@ -179,14 +179,18 @@ def prepare(engine, X, group=None, shard: str = "auto"):
 
 
 def _uses_graph(graph, world, group, split):
-    """HIP-graph replay of the multi-GPU iteration sequence: opt-in (``graph=True``
-    or ``PCM_LLOYD_GRAPH=1``) and only with RCCL, whose collectives can be
-    captured (gloo's cannot)."""
+    """HIP-graph replay of the multi-GPU iteration sequence: on by default with
+    RCCL, whose collectives can be captured (gloo's cannot); ``graph=False`` or
+    ``PCM_LLOYD_GRAPH=0`` launches eagerly.  Round 5 made it the default: the
+    captured sequence (k_lloyd1, all-reduce, update) is what ``bench.py --gpus N``
+    measures, a refused capture falls back to eager launches on every rank
+    (``agree``), and the eager sequence pays a host round trip per chunk plus
+    the launch gaps around every collective (``profiles/rd5_split_graph_vs_eager.txt``)."""
     import os
 
     import torch.distributed as dist
     if graph is None:
-        graph = os.environ.get("PCM_LLOYD_GRAPH", "0") == "1"
+        graph = os.environ.get("PCM_LLOYD_GRAPH", "1") != "0"
     if not graph or not (world > 1 or split) or not dist.is_initialized():
         return False
     try:
@@ -213,7 +217,7 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, gra
     One process: ``pcm_iterate`` (k_lloyd + fused k_step per iteration).  Several
     (or ``split``): ``iter_local`` (k_lloyd accumulating into the statistics
     buffer) -> all-reduce of the statistics (only when world > 1) ->
-    ``iter_global`` (k_step on them).  With RCCL and ``graph`` (opt-in, see
+    ``iter_global`` (k_step on them).  With RCCL (and ``graph`` not False, see
     ``_uses_graph``) a chunk of that sequence is captured once in a HIP graph and replayed: no host launch
     gaps between the kernels and the collective; the device control block gates
     iterations queued past convergence or a halt either way."""
