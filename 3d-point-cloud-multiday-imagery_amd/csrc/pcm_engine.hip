@@ -58,7 +58,6 @@ struct pcm_engine {
     long long ntiles = 0;            // host copy: -1 = not read back yet (pcm_layout_info reads it)
     long long ntiles_cap = 0;        // upper bound on the tiles of the current layout (grid sizing)
     uint32_t tile_cap = TILE;        // points per tile
-    uint32_t tile_cap_big = TILE_BIG;   // ... in cells single-signed on every axis (cell_tile_cap)
     uint32_t *ntiles_host = nullptr; // pinned: the layout's tile count, read back at the end of pcm_layout_build
     // device buffers (persistent: grown on demand, reused by later layouts, freed at destroy)
     void *xs = nullptr;
@@ -344,21 +343,6 @@ void make_grid(Grid &g, int d, const double *lo, const double *hi, double target
     g.prune = (maxext < 1e18) ? 1 : 0;
 }
 
-// Assign blocks (the fine-grid k_lloyd1 instance: 8 lane slots, no masks) the
-// chip holds at once, from the occupancy API.
-int lloyd1_resident(const pcm_engine *e) {
-    int per_cu = 0;
-    const int rc = dispatch_td(e->dtype, e->d, [&](auto T, auto DD) -> int {
-        using TT = decltype(T);
-        constexpr int D = decltype(DD)::value;
-        const size_t lds = (size_t)AccL<D, 8>::words * sizeof(uint32_t);
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_lloyd1<TT, D, 8, false>, TPB,
-                                                            lds) == hipSuccess ? 0 : 1;
-    });
-    if (rc || per_cu < 1) return 0;
-    return per_cu * e->num_cu;
-}
-
 // The Lloyd engine's pruning grid: about min(32 K, n / 2800) cells -- ~2.8k
 // points per cell: fewer, fuller tiles (a tile round is 1024 points) outweigh
 // the slightly longer candidate lists (swept on 12.5M / 100M clouds).
@@ -372,26 +356,8 @@ void choose_grid(pcm_engine *e) {
     const double share = e->n_global > 0 ? std::min(1.0, (double)e->n / (double)e->n_global) : 1.0;
     const double per_centre = e->d >= 4 ? 48.0 : 32.0;
     double target = std::min(per_centre * e->k * share, (double)e->n / (e->d >= 4 ? 1000.0 : 2800.0));
-    // One generation (round 5): when the cells would outnumber the assign blocks
-    // the chip holds at once but the cloud fits that many tiles of <= ~0.6 TILE_BIG
-    // points (an 8-way config-4 slab: 12.5M points, 4096 cells = ~1.4 generations,
-    // whose second one costs a whole block lifetime), take fewer, fuller cells so
-    // that every tile's block starts at once.
-    const double fill = [] { const char *v = std::getenv("PCM_ONEGEN_FILL"); return v ? std::atof(v) : 0.85; }();
-    const double resident = fill * (double)lloyd1_resident(e);
-    bool onegen = false;
-    if (e->d <= 3 && fill > 0.0 && e->tile_cap_big > e->tile_cap && resident >= 1.0 && target > resident &&
-        (double)e->n <= 0.6 * TILE_BIG * resident) {
-        target = resident;
-        onegen = true;
-    }
     if (const char *ov = std::getenv("PCM_CELL_TARGET")) target = std::atof(ov);   // tuning sweeps only
     make_grid(e->g, e->d, e->lo, e->hi, target);
-    // make_grid rounds each axis: shrink the target until the cells fit the generation
-    for (int it = 0; onegen && it < 16 && (double)e->g.ncells > resident; ++it) {
-        target *= 0.95;
-        make_grid(e->g, e->d, e->lo, e->hi, target);
-    }
     if (e->k <= 1) e->g.prune = 0;
 }
 
@@ -666,9 +632,6 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     // the assign kernel addresses points with 32-bit offsets and uses offset
     // 0x0ffffff0 (points) as its always-out-of-range prefetch
     if (e->npad >= 0x0ffffff0LL) return fail(PCM_E_ARG, "at most 2^28 - 32 points per engine (shard larger clouds)");
-    // points per tile of single-signed cells (PCM_TILE_BIG=0 keeps TILE everywhere: A/B only)
-    static const bool big_on = [] { const char *v = std::getenv("PCM_TILE_BIG"); return !(v && std::atoi(v) == 0); }();
-    e->tile_cap_big = big_on ? (uint32_t)TILE_BIG : (uint32_t)TILE;
     choose_grid(e);
     const long long nc = e->g.ncells;
     const size_t ts = tsize(e->dtype);
@@ -679,9 +642,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         return (uint32_t)std::min(TILE, std::max(4 * TPB, c));
     }();
     e->tile_cap = tcap;
-    if (tcap < (uint32_t)TILE) e->tile_cap_big = tcap;
-    // every cell holds ceil(count / cap) <= count / cap + 1 tiles (single-signed
-    // cells fewer: up to TILE_BIG points each)
+    // every cell holds ceil(count / cap) <= count / cap + 1 tiles
     e->ntiles_cap = nc + n / e->tile_cap + 1;
     e->ntiles = -1;
 
@@ -774,27 +735,16 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
         k_cell_from_sub<<<blocks_for(nc + 1), 256, 0, s>>>(e->sub_start, nc, sh, e->cell_start);
         LAUNCHCHK();
     }
-    if (int rc2 = dispatch_d(e->d, [&](auto DD) -> int {
-            constexpr int D = decltype(DD)::value;
-            k_tile_counts<D><<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap, e->tile_cap_big, e->g);
-            LAUNCHCHK();
-            return 0;
-        }))
-        return rc2;
+    k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap);
+    LAUNCHCHK();
     LAUNCHCHK();
     size_t sb = scan_bytes;
     if (rocprim::exclusive_scan(tmp, sb, tcnt, e->tile_off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s) != hipSuccess)
         return fail(PCM_E_HIP, "layout: tile scan");
     k_tile_total<<<1, 64, 0, s>>>(e->tile_off, tcnt, nc, e->ntiles_dev);
     LAUNCHCHK();
-    if (int rc2 = dispatch_d(e->d, [&](auto DD) -> int {
-            constexpr int D = decltype(DD)::value;
-            k_tile_write<D><<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles, e->tile_cap,
-                                                           e->tile_cap_big, e->g);
-            LAUNCHCHK();
-            return 0;
-        }))
-        return rc2;
+    k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles, e->tile_cap);
+    LAUNCHCHK();
     // the exact tile count for the grids of the per-tile kernels (the bound
     // ntiles_cap launched ~1.7x as many blocks at config 3, the excess exiting
     // after one memory latency: a drain tail on every assign launch)
@@ -1778,7 +1728,7 @@ int pcm_debug_kpp_counts(unsigned long long *out, int ncentres) {
     return 0;
 }
 int pcm_debug_timing_lloyd(unsigned long long *out, int nblocks) {
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_l), (size_t)nblocks * 4 * sizeof(unsigned long long)));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_l), (size_t)nblocks * 8 * sizeof(unsigned long long)));
     return 0;
 }
 #endif

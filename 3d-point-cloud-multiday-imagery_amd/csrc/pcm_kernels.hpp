@@ -29,12 +29,6 @@ constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-
 #endif
 constexpr int TPB = PCM_TPB;       // assign block size
 constexpr int TILE = 32 * TPB;     // max points per tile: <= 32 per lane, 64 per shared LDS word (see AccL)
-// Tiles of cells that are single-signed on every axis may hold up to TILE_BIG
-// points (round 5): a shared LDS word then sums <= 128 values of one known sign,
-// |sum| < 2^32, recovered exactly from the word read as unsigned (k_lloyd1's
-// fold, cell_signs).  Fewer, fuller tiles let a small slab's launch fit in one
-// generation of resident blocks (choose_grid).
-constexpr int TILE_BIG = 64 * TPB;
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int TLCAP = 256;        // tile lists staged whole in k_lloyd1's LDS (slot-map path)
 constexpr int TLMAX = 1024;       // tile-list capacity (longer lists: FULL); lists past TLCAP scan in LDS chunks
@@ -318,46 +312,12 @@ __device__ __forceinline__ long long xs_index(long long i, int a) {
     return ((i >> 2) * D + a) * 4 + (i & 3);
 }
 
-// Sign of every axis over a cell: 2 bits per axis, 1 = every point binned there
-// is >= 0 (the cell box's lower edge, binning fuzz included, is >= 0), 2 = every
-// point <= 0, 0 = the cell may hold both signs.  -0.0 counts as either: its
-// fixed-point value is 0.
-template <int D>
-__device__ __forceinline__ unsigned cell_signs(const Grid &g, unsigned cell) {
-    int ci[MAXD];
-    for (int a = D - 1, c = (int)cell; a >= 0; --a) {   // cell ids fit 32 bits (sort keys)
-        ci[a] = (int)((unsigned)c % (unsigned)g.G[a]);
-        c = (int)((unsigned)c / (unsigned)g.G[a]);
-    }
-    double blo[MAXD], bhi[MAXD];
-    cell_box<D>(g, ci, ci, blo, bhi);
-    unsigned m = 0u;
-#pragma unroll
-    for (int a = 0; a < D; ++a) m |= (blo[a] >= 0.0 ? 1u : (bhi[a] <= 0.0 ? 2u : 0u)) << (2 * a);
-    return m;
-}
-template <int D>
-__device__ __forceinline__ bool cell_single_signed(unsigned m) {
-    bool ok = true;
-#pragma unroll
-    for (int a = 0; a < D; ++a) ok = ok && ((m >> (2 * a)) & 3u) != 0u;
-    return ok;
-}
-// points per tile of cell c: capbig when the cell is single-signed on every axis
-template <int D>
-__device__ __forceinline__ uint32_t cell_tile_cap(const Grid &g, unsigned c, uint32_t cap, uint32_t capbig) {
-    return (capbig > cap && cell_single_signed<D>(cell_signs<D>(g, c))) ? capbig : cap;
-}
-
-template <int D>
 __global__ __launch_bounds__(256) void k_tile_counts(const uint32_t *__restrict__ start, long long ncells,
-                                                     uint32_t *__restrict__ cnt, uint32_t cap, uint32_t capbig,
-                                                     Grid g) {
+                                                     uint32_t *__restrict__ cnt, uint32_t cap) {
     long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (c >= ncells) return;
-    const uint32_t n = start[c + 1] - start[c];
-    const uint32_t cp = cell_tile_cap<D>(g, (unsigned)c, cap, capbig);
-    cnt[c] = (n + cp - 1) / cp;
+    uint32_t n = start[c + 1] - start[c];
+    cnt[c] = (n + cap - 1) / cap;
 }
 
 // tile_off[nc] and the tile count (the scan is exclusive: add the last cell's count)
@@ -369,17 +329,14 @@ __global__ void k_tile_total(uint32_t *__restrict__ off, const uint32_t *__restr
     *ntiles = t;
 }
 
-template <int D>
 __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__ start, const uint32_t *__restrict__ off,
-                                                    long long ncells, uint4 *__restrict__ tiles, uint32_t cap,
-                                                    uint32_t capbig, Grid g) {
+                                                    long long ncells, uint4 *__restrict__ tiles, uint32_t cap) {
     long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (c >= ncells) return;
     uint32_t s = start[c], e = start[c + 1];
     uint32_t n = e - s;
     if (n == 0) return;
-    const uint32_t cp = cell_tile_cap<D>(g, (unsigned)c, cap, capbig);
-    uint32_t nt = (n + cp - 1) / cp;
+    uint32_t nt = (n + cap - 1) / cap;
     uint32_t per = (n + nt - 1) / nt;
     uint32_t o = off[c];
     for (uint32_t t = 0; t < nt; ++t) {
@@ -431,10 +388,10 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
     const uint4 tr = tiles[t];
     const unsigned start = tr.y, end = tr.z;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    // the whole tile (<= TILE_BIG = 32 x 256 points) in registers: every load in
+    // the whole tile (<= TILE = 16 x 256 points) in registers: every load in
     // flight at once, one read of xs (a strided loop waited one latency per
     // round, twice: 505-530 us for 100M points)
-    constexpr int PPT = TILE_BIG / 256;
+    constexpr int PPT = TILE / 256;
     unsigned bits[PPT][3];
 #pragma unroll
     for (int u = 0; u < PPT; ++u) {
@@ -706,8 +663,10 @@ constexpr int CAND_MAXCH = 64;           // pair path: children per block
 __device__ unsigned long long g_dbg_t[8192][16];
 #define DBG_T(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define DBG_V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = (unsigned long long)(v); } while (0)
-__device__ unsigned long long g_dbg_l[65536][4];
+__device__ unsigned long long g_dbg_l[65536][8];
 #define DBG_L(k) do { if (threadIdx.x == 0 && blockIdx.x < 65536) g_dbg_l[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// k_lloyd1 block info: [5] HW_ID (cu/sh/se), [6] XCC_ID, [7] list length | tile points << 16
+#define DBG_LV(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 65536) g_dbg_l[blockIdx.x][k] = (unsigned long long)(v); } while (0)
 __device__ unsigned long long g_dbg_e[8192][8];
 // k-means++ per-step work counters [centre][eval items, eval reached cells, apply items, apply reached]
 __device__ unsigned long long g_dbg_kpp[4096][4];
@@ -721,6 +680,7 @@ __device__ unsigned long long g_dbg_kpp[4096][4];
 #define DBG_T(k) do { } while (0)
 #define DBG_V(k, v) do { } while (0)
 #define DBG_L(k) do { } while (0)
+#define DBG_LV(k, v) do { } while (0)
 #endif
 
 // Wave-wide minimum through DPP (row_shr 1/2/4/8 scan, then row_bcast 15/31;
@@ -1675,6 +1635,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     asm volatile("" : "+s"(zm.x), "+s"(zm.y), "+s"(zm.z), "+s"(zm.w));
     if (gate != 0u || t >= nt) return;
     DBG_L(0);
+    DBG_LV(5, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));    // HW_REG_HW_ID, 32 bits
+    DBG_LV(6, __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)));   // HW_REG_XCC_ID, 16 bits
     const unsigned cell = tr.x, start = tr.y, end = tr.z;
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f);
     int l0 = 0;
@@ -1683,6 +1645,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
         l0 = fc_lab[(size_t)cell * CAPF + tid];
     }
     uint32_t cnt = fc_cnt[cell];
+    DBG_LV(7, (unsigned long long)(cnt & 0xFFFFu) | ((unsigned long long)(end - start) << 16));
     // crowded cell (list FULL or past TL_MIN): the tile's own list when k_tile_cand built a shorter one
     // (lists past TLCAP and all-K scans go through LDS in chunks, below)
     const float4 *lrec = fc_rec + (size_t)cell * CAPF;
@@ -1703,10 +1666,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     for (int o = 0; o <= NSUB; ++o) ss[o] = (MASK && A.sub) ? A.sub_start[((size_t)cell << D) + o] : 0u;
     const unsigned base0 = start & ~3u;
     const int nr = (int)((end - base0 + 4 * TPB - 1) / (4 * TPB));
-    // a tile longer than TILE (<= TILE_BIG: single-signed cells only, k_tile_write)
-    // puts up to 128 values in a shared LDS word: its fold reads coordinate words
-    // by the cell's per-axis sign (cell_signs), else as int32
-    const unsigned sgn = (end - start > (unsigned)TILE) ? cell_signs<D>(A.g, cell) : 0u;
     const rsrc_t rx = make_rsrc(A.xs, (unsigned long long)A.npad * D * sizeof(T));
     // compressed tile (k_tile_compress): 8-B records from xz, decoded exactly
     const bool zc = ZOK && (zm.w >> 31);
@@ -1722,7 +1681,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
     };
     __shared__ unsigned long long omask[NSUB];
     __shared__ uint32_t okey[NSUB];
-    __shared__ unsigned long long rmask[TILE_BIG / (4 * TPB) + 1];   // rounds of one tile
+    __shared__ unsigned long long rmask[TILE / (4 * TPB) + 1];   // rounds of one tile
     // The rest of the kernel, instantiated per point format: compressed tiles
     // (fp32 D = 3, 8-B records) issue 2 b128 loads per work item, raw tiles
     // D * sizeof(T) / 4 -- one constant load count per instance keeps hipcc's
@@ -2059,7 +2018,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             }
         }
     };
-    // PF+1 rotating register sets; a tile spans at most TILE_BIG / (4 TPB) + 1 = 17 rounds
+    // PF+1 rotating register sets; a tile spans at most TILE / (4 TPB) + 1 = 9 rounds
     for (int r = 0; r < nr; r += PF + 1) {
 #pragma unroll
         for (int k = 0; k <= PF; ++k) step(xr[k], xr[(k + PF) % (PF + 1)], r + k);
@@ -2074,15 +2033,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<
             const int pi = p0 + tid / 16, sub = tid & 15;
             long long sacc = 0;
             if (pi < npairs) {
-                const int qa = pi % (D + 1);
-                // word mode: 0 int32 (tiles <= TILE), 1 unsigned (counts; axes >= 0 of a
-                // longer tile), 2 non-positive axis of a longer tile (sum in (-2^32, 0])
-                const unsigned md = (qa == D) ? 1u : ((sgn >> (2 * qa)) & 3u);
+                const bool isc = (pi % (D + 1) == D);
                 const uint32_t *row = acc + pi * AW;
                 for (int k = 0; k < AW / 16; ++k) {
                     const uint32_t w = row[sub + 16 * k];
-                    sacc += md == 0u ? (long long)(int32_t)w
-                                     : (md == 1u ? (long long)w : (w ? (long long)w - (1ll << 32) : 0ll));
+                    sacc += isc ? (long long)w : (long long)(int32_t)w;
                 }
             }
             sacc += __shfl_down(sacc, 8, 16);
@@ -2470,11 +2425,14 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
         __hip_atomic_store(&pp->smax_bits, (unsigned long long)__double_as_longlong(ds), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // release: this block's sh[] and record stores are ordered before its arrival
+        // (the HIP memory model's contract; the sc1 stores above are drained anyway)
+        const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (prior == gridDim.x - 1) ? 1u : 0u;
     }
     __syncthreads();
     if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every other block's published stores are visible
     // ---- the last block: every other block's sh[] and record have landed
     unsigned long long changed = 0ull, n_empty = 0ull;
     double dmax = 0.0, smax = 0.0;
@@ -2736,6 +2694,7 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     float4 *__restrict__ fc_rec, int32_t *__restrict__ fc_lab, int bpc) {
     static_assert(R * CAND_TPB <= SHIFT_LANES && SHIFT_LANES % CAND_TPB == 0, "one tree lane per row");
     extern __shared__ __attribute__((aligned(16))) float4 cstage[];   // the K new centres
+    DBG_T(13);
     unsigned gate = ctrl->halt | ctrl->done;
     const uint32_t it = ctrl->iter, max_iter = ctrl->max_iter;
     const unsigned sel = ctrl->ref_sel;
@@ -2762,6 +2721,7 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
         }
     }
     if (gate != 0u) return;
+    DBG_T(0);
     const unsigned par = it & 1u;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -2801,7 +2761,8 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     if (lane == 0) { s_neq[wv] = neq; s_ne[wv] = ne; s_dr[wv] = dr; s_ds[wv] = ds; }
     __syncthreads();   // every load of this block has returned (its values are used above)
     if (tid == 0) {
-        const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // release: this block's loads of the rows the publisher overwrites are ordered before its arrival
+        const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (prior == gridDim.x - 1) ? 1u : 0u;
     }
     unsigned long long changed = 0ull, n_empty = 0ull;
@@ -2815,7 +2776,9 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     double dl_new = alpha * sqrt(smax) * slack;
     if (!(dl_new <= dl_cap)) dl_new = 0.0;
     __syncthreads();   // s_last
+    DBG_T(15);
     if (s_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         // ---- the publisher: every other block's loads have returned
         unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
 #pragma unroll
@@ -2868,6 +2831,7 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
         }
     }
     if (n_empty > 0ull) return;   // halted: the lists stay (resume rebuilds them)
+    DBG_T(14);
     // this block's cells: rebuilt at the new centres with the new budget, or refreshed
     if (rebuild) cand_body<D, 4>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new, CoarseL{});
     else refresh_body<D>(g, cstage, fc_cnt, fc_rec, fc_lab);

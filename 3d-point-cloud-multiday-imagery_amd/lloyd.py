@@ -76,19 +76,24 @@ def slab_sizes(hist: np.ndarray, owner: np.ndarray, world: int) -> np.ndarray:
                        minlength=world).astype(np.int64)
 
 
-def _build_all(engine, X, q, gidx0, world, group):
-    """engine.build on every rank; a failure on any rank raises on every rank
-    (MIN all-reduce of an ok flag), so no rank is left waiting in the next
-    collective."""
-    err = None
+def _agreed(fn, what, world, group, device):
+    """fn() on every rank; a failure on any rank raises on every rank (MIN
+    all-reduce of an ok flag), so no rank is left waiting in the next collective."""
+    err, out = None, None
     try:
-        engine.build(X, q, gidx0)
+        out = fn()
     except Exception as exc:   # noqa: BLE001 -- re-raised below, after the ranks agree
         err = exc
-    if not agree(err is None, world, group, engine.stats_device):
+    if not agree(err is None, world, group, device):
         if err is not None:
             raise err
-        raise RuntimeError("pcm_amd.lloyd: the layout build failed on another rank")
+        raise RuntimeError(f"pcm_amd.lloyd: {what} failed on another rank")
+    return out
+
+
+def _build_all(engine, X, q, gidx0, world, group):
+    """engine.build on every rank, failures agreed (``_agreed``)."""
+    _agreed(lambda: engine.build(X, q, gidx0), "the layout build", world, group, engine.stats_device)
 
 
 def slab_owner(hist: np.ndarray, world: int) -> np.ndarray:
@@ -159,19 +164,24 @@ def prepare(engine, X, group=None, shard: str = "auto"):
         warnings.warn("pcm_amd.lloyd: a spatial slab would exceed one engine's capacity; keeping row shards")
         _build_all(engine, X, q, gidx0, world, group)
         return q, n_total
-    Xs, rows, send = engine.shard_partition(X, axis, glo[axis], inv, SLAB_BINS, owner, world, gidx0)
+    # every step that can fail on one rank alone (a partition workspace or a receive
+    # buffer out of memory on a skewed rank) is agreed before the next collective
+    sdev = engine.stats_device
+    Xs, rows, send = _agreed(lambda: engine.shard_partition(X, axis, glo[axis], inv, SLAB_BINS, owner, world, gidx0),
+                             "the slab partition", world, group, sdev)
     st = torch.tensor(send, dtype=torch.int64, device=dev)
     rt = torch.empty_like(st)
     dist.all_to_all_single(rt, st, group=group)
     recv = rt.cpu().numpy().astype(np.int64)
     sl, rl = [int(v) for v in send], [int(v) for v in recv]
-    Xr = torch.empty((sum(rl), d), dtype=X.dtype, device=X.device)
+    Xr, rows_r = _agreed(lambda: (torch.empty((sum(rl), d), dtype=X.dtype, device=X.device),
+                                  torch.empty(sum(rl), dtype=torch.int32, device=X.device)),
+                         "the slab receive buffers", world, group, sdev)
     dist.all_to_all_single(Xr, Xs, rl, sl, group=group)
-    rows_r = torch.empty(sum(rl), dtype=torch.int32, device=X.device)
     dist.all_to_all_single(rows_r, rows, rl, sl, group=group)
     del Xs
-    engine.bbox(Xr)
-    engine.set_shard(rows_r, n_total)
+    _agreed(lambda: (engine.bbox(Xr), engine.set_shard(rows_r, n_total)), "the slab bounding box", world, group,
+            sdev)
     _build_all(engine, Xr, q, 0, world, group)
     engine._slab = dict(rows=rows, send=sl, recv=rl, gidx0=gidx0, n_local=n_local, axis=axis,
                         n_slab=sum(rl))

@@ -49,6 +49,10 @@ def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False, sha
         def bad_build(*args, **kw):
             raise RuntimeError("injected build failure")
         eng.build = bad_build
+    if opts.get("fail_partition_rank") == rank:
+        def bad_partition(*args, **kw):
+            raise MemoryError("injected partition failure")
+        eng.shard_partition = bad_partition
     try:
         res = pcm_amd.lloyd_fit(torch.from_numpy(X[a:b]), torch.from_numpy(C0), max_iter=max_iter, tol=0.0,
                                 chunk=chunk, engine=eng, group=L.LOCAL if local else None, shard=shard)
@@ -203,3 +207,14 @@ def test_build_failure_on_one_rank_raises_on_every_rank(tmp_path):
         parts = run_world(X, C0, 5, 4, tmp_path, shard=shard, opts={"fail_build_rank": 1})
         assert "injected build failure" in str(parts[1]["error"])
         assert "another rank" in str(parts[0]["error"])
+
+
+def test_partition_failure_on_one_rank_raises_on_every_rank(tmp_path):
+    """the slab partition (its workspace) failing on rank 1 only: both
+    ranks raise before the all_to_all instead of rank 0 blocking in it."""
+    from oracle import lloyd_ref as R
+    X = R.splitmix_uniform(3000, 3, 28)
+    C0 = X[R.init_indices(3000, 8)]
+    parts = run_world(X, C0, 5, 4, tmp_path, shard="slab", opts={"fail_partition_rank": 1})
+    assert "injected partition failure" in str(parts[1]["error"])
+    assert "another rank" in str(parts[0]["error"])

@@ -99,9 +99,8 @@ def test_crowded_2d_and_f16(pcm, monkeypatch):
 
 @pytest.mark.parametrize("name,zlev,k,expect", [
     ("many", "auto", 4096, "long"),       # tile lists of 257..1024 entries: LDS chunks, carried bd/bj
-    ("many", "1", 1024, "any"),           # one Morton level: a tile spans most of its cluster
-    ("clusters", "1", 4096, "allk"),      # ... -> lists past 1024 -> all-K tiles
-    ("clusters", "1", 1024, "any"),
+    ("clusters", "1", 4096, "allk"),      # one Morton level: a tile spans its whole cluster -> past 1024 -> all K
+    ("clusters", "1", 1024, "any"),       # ~512 centres per cluster: lists past 256
 ])
 def test_crowded_long_lists_and_allk_tiles(pcm, name, zlev, k, expect, monkeypatch):
     """the chunked crowded path of k_lloyd1 (tile lists longer than TLCAP = 256,

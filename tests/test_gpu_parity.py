@@ -364,3 +364,9 @@ def test_update_paths_d4(pcm):
     C0[60:90] = C0[0]
     ref = R.lloyd_fit(X, C0, max_iter=8, fast=True)
     assert_same(gpu_fit(pcm, X, C0, 8, dtype=torch.float16), ref, f"fused={fused} d4 relocation")
+    # K > 2048 (the multi-block k_upd with its release/acquire hand-off) through a relocation
+    # (ADVICE r4): 40 duplicated centres leave 39 clusters empty at the first update
+    C0 = X[R.init_indices(X.shape[0], 3000)].copy()
+    C0[2000:2040] = C0[5]
+    ref = R.lloyd_fit(X, C0, max_iter=6, fast=True)
+    assert_same(gpu_fit(pcm, X, C0, 6, dtype=torch.float16), ref, f"fused={fused} d4 k=3000 relocation")

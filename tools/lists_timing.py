@@ -14,7 +14,8 @@ rest = sys.argv[3:]
 N, K, D = (int(v) for v in rest[:3])
 pdt = torch.float16 if "f16" in rest else torch.float32
 P = int(rest[rest.index("slab") + 1]) if "slab" in rest else 1
-os.environ.setdefault("PCM_FUSED_UPD", "0")   # D <= 3: time k_lists, not the fused kernel
+FUSED = "fused" in sys.argv[3:]
+os.environ.setdefault("PCM_FUSED_UPD", "1" if FUSED else "0")   # D <= 3: k_lists, or (fused) k_updlists
 X = synth_uniform(N, D, seed=0, start=0).to(pdt)
 C0 = synth_rows(np.sort(np.random.default_rng(1).choice(N, K, replace=False)), D, seed=0).to(pdt).float()
 eng = Engine(D, K, pdt, max_iter=50)
@@ -46,8 +47,11 @@ t0 = t[:, 0].min()
 us = lambda v: np.asarray(v) / 100.0   # s_memrealtime: 100 MHz
 print(f"N={N} K={K} D={D} slab {P}: iters {st['iter']} rebuilds {st['list_rebuilds']} blocks {len(t)} "
       f"layout {eng.layout_info()} lists {eng.candidate_stats()}")
-print("block start rel. first us: p50 %.1f p90 %.1f max %.1f" % tuple(us(np.percentile(t[:, 0] - t0, q)) for q in (50, 90, 100)))
-for k0, k1, name in ((0, 4, "list source + reference"), (4, 5, "prune bits"), (5, 1, "compaction"), (1, 10, "children boxes"),
+t0 = t[:, 13].min() if FUSED else t0
+print("block start rel. first us: p50 %.1f p90 %.1f max %.1f" % tuple(us(np.percentile(t[:, 13 if FUSED else 0] - t0, q)) for q in (50, 90, 100)))
+for k0, k1, name in ((13, 0, "fused: control + rows (one latency)"), (0, 15, "fused: centres + arrival"),
+                     (15, 14, "fused: publisher / decisions"), (14, 4, "fused: -> list reference"),
+                     (0, 4, "list source + reference"), (4, 5, "prune bits"), (5, 1, "compaction"), (1, 10, "children boxes"),
                      (10, 11, "pair A (refs)"), (11, 12, "pair B (prune)"), (12, 2, "pair C (write)"), (0, 2, "block total")):
     ok = (t[:, k0] > 0) & (t[:, k1] > 0)
     if ok.any():

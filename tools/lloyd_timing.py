@@ -38,17 +38,20 @@ eng.iterate(iters); torch.cuda.synchronize()
 lib = _lib.load()
 lib.pcm_debug_timing_lloyd.argtypes = [ctypes.c_void_p, ctypes.c_int]
 nb = 65536
-buf = np.zeros((nb, 4), np.uint64)
+buf = np.zeros((nb, 8), np.uint64)
 assert lib.pcm_debug_timing_lloyd(buf.ctypes.data_as(ctypes.c_void_p), nb) == 0
 t = buf.astype(np.int64)
 t = t[t[:, 0] > 0]
+# columns: 0 record in (after the block's first memory latency), 1 first round, 2 rounds done,
+# 3 end, 5 HW_ID, 6 XCC_ID, 7 list length | tile points << 16 (a stamp before the first loads
+# trips hipcc: "illegal VGPR to SGPR copy")
 t0 = t[:, 0].min()
 us = lambda v: np.asarray(v) / 100.0   # s_memrealtime: 100 MHz
 info = eng.layout_info()
 print(f"N={N} K={K} D={D} {pdt} slab {P} (rank 0: {int(eng.n)} points, cells {info['ncells']}, tiles "
       f"{info['ntiles']}, kernel {eng.assign_kernel()}, lists {eng.candidate_stats()}) blocks {len(t)} "
       f"kernel span {us(t[:, 3].max() - t0):.1f} us")
-for name, a, b in (("start (rel. first)", None, 0), ("setup (start->first round)", 0, 1), ("rounds", 1, 2),
+for name, a, b in (("start (rel. first)", None, 0), ("setup (record->first round)", 0, 1), ("rounds", 1, 2),
                    ("fold+exit", 2, 3), ("block total", 0, 3), ("end (rel. first start)", None, 3)):
     v = t[:, b] - (t0 if a is None else t[:, a])
     print("%-28s p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f us" % ((name,) + tuple(us(np.percentile(v, q)) for q in (10, 50, 90, 100))))
@@ -58,3 +61,27 @@ occ = np.zeros(span + 1)
 for s_, e_ in zip(us(t[:, 0] - t0).astype(int), us(t[:, 3] - t0).astype(int)):
     occ[s_:e_ + 1] += 1
 print("resident blocks per us bin:", " ".join(str(int(x)) for x in occ[::max(1, span // 40)]))
+
+# what the slow blocks have in common: block time by XCC, shader engine, list length, tile size, start time
+tot = us(t[:, 3] - t[:, 0])
+rnd = us(t[:, 2] - t[:, 1])
+xcc = t[:, 6] & 0xF
+se = (t[:, 5] >> 13) & 0x7
+mm = t[:, 7] & 0xFFFF
+ln = (t[:, 7] >> 16) & 0xFFFF
+st = us(t[:, 0] - t0)
+def by(name, key, vals):
+    out = []
+    for v in vals:
+        m = key == v
+        if m.sum():
+            out.append(f"{v}:{tot[m].mean():.1f}/{rnd[m].mean():.1f}({m.sum()})")
+    print(f"block total/rounds mean by {name}: " + " ".join(out))
+by("xcc", xcc, range(8))
+by("se", se, range(8))
+by("list len", np.minimum(mm, 12), range(13))
+q = np.quantile(ln, [0.0, 0.25, 0.5, 0.75, 1.0])
+by("tile pts quartile", np.searchsorted(q[1:-1], ln), range(4))
+by("start us//4", np.minimum(st // 4, 12).astype(int), range(13))
+print("corr(total, list len) %.2f  corr(total, tile pts) %.2f  corr(rounds, start) %.2f" % (
+    np.corrcoef(tot, mm)[0, 1], np.corrcoef(tot, ln)[0, 1], np.corrcoef(rnd, st)[0, 1]))
