@@ -1209,14 +1209,20 @@ int pcm_time_assign(pcm_engine *e, int reps, void *stream, double *ms) {
     return 0;
 }
 
-// Single-process iterations: k_lloyd1 into partials[parity], k_upd, k_lists.
+// Single-process iterations: the multi-GPU sequence without the all-reduce --
+// k_lloyd1 into the statistics buffer, then the update reading it in place (its
+// publisher zeroes it once every block has read it).  Round 5: the parity halves
+// of `partials` that the single-GPU path used before made every k_updlists block
+// load both halves (the parity is a device control word): 32 of its 144 B per
+// centroid row, all blocks, from L2.  PCM_PARITY_ITER=1 keeps the old path (A/B).
 int pcm_iterate(pcm_engine *e, int n, void *stream) {
     if (!e || n < 0) return fail(PCM_E_ARG, "bad argument");
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
     hipStream_t s = (hipStream_t)stream;
+    static const bool parity = [] { const char *v = std::getenv("PCM_PARITY_ITER"); return v && std::atoi(v) == 1; }();
     for (int i = 0; i < n; ++i) {
-        if (int rc = iter_local_impl(e, s, false)) return rc;   // parity halves of `partials`
-        if (int rc = iter_global_impl(e, s, true, false)) return rc;
+        if (int rc = iter_local_impl(e, s, !parity)) return rc;
+        if (int rc = iter_global_impl(e, s, parity, false)) return rc;
     }
     return 0;
 }

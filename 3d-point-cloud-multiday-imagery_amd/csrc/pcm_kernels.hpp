@@ -75,6 +75,16 @@ struct Ctrl {
     alignas(128) unsigned long long inert_rep[INERT_REP][16];
 };
 
+// Arrival of block blockIdx.x among gridDim.x on one counter: true for the last
+// one.  Release: the block's prior loads and stores precede its arrival (the
+// last block then takes an acquire fence).  Round 5 measured a two-level
+// arrival (8 group counters, then one) at config 3: "centres + arrival" 6.2 ->
+// 7.3 us per block, so the single counter stays (profiles/rd5_updlists_phases_c3.txt).
+__device__ __forceinline__ bool arrive_last(Ctrl *ctrl) {
+    const unsigned p = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return p == gridDim.x - 1u;
+}
+
 // Fixed-point exponents q_a (identical on every rank).
 struct QExp {
     int q[MAXD];
@@ -2425,10 +2435,9 @@ __global__ __launch_bounds__(UPD_TPB) void k_upd(unsigned long long *__restrict_
         __hip_atomic_store(&pp->smax_bits, (unsigned long long)__double_as_longlong(ds), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // release: this block's sh[] and record stores are ordered before its arrival
-        // (the HIP memory model's contract; the sc1 stores above are drained anyway)
-        const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (prior == gridDim.x - 1) ? 1u : 0u;
+        // release (arrive_last): this block's sh[] and record stores are ordered
+        // before its arrival (the sc1 stores above are drained anyway)
+        s_last = arrive_last(ctrl) ? 1u : 0u;
     }
     __syncthreads();
     if (!s_last) return;
@@ -2760,11 +2769,8 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     __shared__ unsigned s_last;
     if (lane == 0) { s_neq[wv] = neq; s_ne[wv] = ne; s_dr[wv] = dr; s_ds[wv] = ds; }
     __syncthreads();   // every load of this block has returned (its values are used above)
-    if (tid == 0) {
-        // release: this block's loads of the rows the publisher overwrites are ordered before its arrival
-        const unsigned prior = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (prior == gridDim.x - 1) ? 1u : 0u;
-    }
+    if (tid == 0)   // release: this block's loads of the rows the publisher overwrites precede its arrival
+        s_last = arrive_last(ctrl) ? 1u : 0u;
     unsigned long long changed = 0ull, n_empty = 0ull;
     double dmax = 0.0, smax = 0.0;
     for (int w = 0; w < NW; ++w) {
