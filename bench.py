@@ -587,7 +587,7 @@ def main():
         # all-reduce (its events include waiting for the slowest rank), the slab size
         mine = torch.tensor([dt, tm["assign_ms"], tm["tail_ms"], tm.get("candidates_ms", 0.0),
                              allreduce_ms if allreduce_ms is not None else -1.0, float(eng.n)],
-                            dtype=torch.float64, device="cuda")
+                            dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
         every = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(every, mine)
         every = torch.stack(every).cpu().numpy()

@@ -44,3 +44,23 @@ def test_launcher_world_must_match_gpus():
 def test_failing_rank_fails_the_launch():
     rc, lines, err = _run("--gpus", "2", "--no-such-flag")
     assert rc != 0
+
+
+def test_report_helpers_cpu():
+    """The bench line's compute roofline and the NumPy-subsample and config-2 CPU legs (CPU only)."""
+    import importlib.util
+    import numpy as np
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    r = bench.compute_roofline(100_000_000, 1024, 3, 2.5, 0.2)
+    assert r["flop_per_point_candidate"] == 10 and abs(r["achieved"] - 1e8 * 2.5 * 10 / 2e-4 / 1e12) < 1e-9
+    assert r["compute_frac"] == r["achieved"] / bench.FP32_PEAK_TFLOPS and r["bruteforce_equivalent"] > r["achieved"]
+    assert bench.compute_roofline(10, 4, 3, 1.0, 0.0) is None
+    from oracle import lloyd_ref as R
+    X = R.splitmix_uniform(20_000, 3, 5)
+    C = X[R.init_indices(20_000, 16)]
+    nb = bench.numpy_baseline(X, C, budget_s=0.02)
+    assert nb["value"] > 0 and nb["kind"] == "port" and "NumPy" in nb["sample"]
+    cb, ref = bench.cpu_fit_baseline(X, C, 5)
+    assert cb["value"] > 0 and ref["n_iter"] <= 5 and ref["labels"].shape == (20_000,)
