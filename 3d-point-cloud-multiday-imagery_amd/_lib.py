@@ -16,7 +16,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 SO_PATH = os.environ.get("PCM_SO") or os.path.join(PKG_DIR, "libpcmkm.so")
 UNITS = [os.path.join(PKG_DIR, "csrc", u) for u in ("pcm_engine.hip", "pcm_dense.hip", "pcm_stereo.hip", "pcm_shard.hip")]
 SOURCES = UNITS + [os.path.join(PKG_DIR, "csrc", h) for h in ("pcm_kernels.hpp", "pcm_kpp.hpp", "pcm_sort.hpp", "pcm_cloud.hpp",
-                                                              "pcm_common.hpp")] + \
+                                                              "pcm_common.hpp", "pcm_debug.hpp")] + \
     [os.path.join(REPO_DIR, "include", "pcm_kmeans.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pcm_debug.hpp"   // DBG_* phase stamps (debug builds only)
+
 namespace pcm {
 
 constexpr int MAXD = 4;
@@ -669,29 +671,6 @@ constexpr int CAND_KBITS = 4096;         // bitmap capacity (larger K: direct ba
 constexpr int CAND_CBW = 512;            // pair path: child bitmap words (4 KB)
 constexpr int CAND_MAXCH = 64;           // pair path: children per block
 
-#ifdef PCM_DBG_TIMING
-__device__ unsigned long long g_dbg_t[8192][16];
-#define DBG_T(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define DBG_V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_t[blockIdx.x][k] = (unsigned long long)(v); } while (0)
-__device__ unsigned long long g_dbg_l[65536][8];
-#define DBG_L(k) do { if (threadIdx.x == 0 && blockIdx.x < 65536) g_dbg_l[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
-// k_lloyd1 block info: [5] HW_ID (cu/sh/se), [6] XCC_ID, [7] list length | tile points << 16
-#define DBG_LV(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 65536) g_dbg_l[blockIdx.x][k] = (unsigned long long)(v); } while (0)
-__device__ unsigned long long g_dbg_e[8192][8];
-// k-means++ per-step work counters [centre][eval items, eval reached cells, apply items, apply reached]
-__device__ unsigned long long g_dbg_kpp[4096][4];
-#define DBG_KPP(c, k, v) do { if ((c) < 4096 && (v)) atomicAdd(&g_dbg_kpp[c][k], (unsigned long long)(v)); } while (0)
-#define DBG_E(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_e[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define DBG_EV(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_dbg_e[blockIdx.x][k] = (unsigned long long)(v); } while (0)
-#else
-#define DBG_E(k) do { } while (0)
-#define DBG_EV(k, v) do { } while (0)
-#define DBG_KPP(c, k, v) do { } while (0)
-#define DBG_T(k) do { } while (0)
-#define DBG_V(k, v) do { } while (0)
-#define DBG_L(k) do { } while (0)
-#define DBG_LV(k, v) do { } while (0)
-#endif
 
 // Wave-wide minimum through DPP (row_shr 1/2/4/8 scan, then row_bcast 15/31;
 // lane 63 ends with the minimum).  The whole wave must be active.  Used only to
