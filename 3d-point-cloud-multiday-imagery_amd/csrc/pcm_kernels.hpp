@@ -82,6 +82,29 @@ struct Ctrl {
 // last block then takes an acquire fence).  Round 5 measured a two-level
 // arrival (8 group counters, then one) at config 3: "centres + arrival" 6.2 ->
 // 7.3 us per block, so the single counter stays (profiles/rd5_updlists_phases_c3.txt).
+// k_updlists' arrival, issued early and read late: a relaxed agent-scope
+// fetch-add by lane 0 of the calling wave (EXEC = lane 0, or no lane when `on`
+// is 0) whose returned value stays in flight -- hipcc's waitcnt pass does not
+// see the asm, and __syncthreads waits only on LDS -- until arrive_read's
+// explicit vmcnt(0).  (The compiler's own atomic would be rewritten into a
+// wave-aggregated form whose broadcast waits for the return on the spot.)
+__device__ __forceinline__ unsigned arrive_issue(unsigned *p, unsigned long long on) {
+    unsigned old = 0u;
+    unsigned long long save;
+    asm volatile(
+        "s_mov_b64 %1, exec\n\t"
+        "s_mov_b64 exec, %4\n\t"
+        "global_atomic_add %0, %2, %3, off sc0\n\t"
+        "s_mov_b64 exec, %1"
+        : "+v"(old), "=&s"(save)
+        : "v"(p), "v"(1u), "s"(on)
+        : "memory");
+    return old;
+}
+__device__ __forceinline__ unsigned arrive_read(unsigned v) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : : "memory");
+    return (unsigned)__builtin_amdgcn_readfirstlane((int)v);
+}
 __device__ __forceinline__ bool arrive_last(Ctrl *ctrl) {
     const unsigned p = __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     return p == gridDim.x - 1u;
@@ -2689,7 +2712,9 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     const double budget = ctrl->budget, tol = ctrl->tol;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = K * (D + 1);
-    // row r of this thread: centroid j = tid + CAND_TPB * r (tree lane j)
+    // row r of this thread: centroid j = tid + CAND_TPB * r (tree lane j).  (The
+    // publisher alone loading the previous rows, for the changed-word count,
+    // measured slower: its extra latency sits on the launch's tail.)
     unsigned long long row[R][D + 1], alt[R][D + 1], pv[R][D + 1];
     float4 rj[R], rk[R], oj[R];
 #pragma unroll
@@ -2721,18 +2746,18 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     unsigned long long neq = 0ull;
     unsigned ne = 0u;
     double dr = 0.0, ds = 0.0, sh[R];
-    float4 cnew[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int j = tid + CAND_TPB * r;
         sh[r] = 0.0;
         if (j < K) {
             double drj = 0.0, dsj = 0.0;
-            upd_row<D>(row[r], pv[r], rj[r], oj[r], qe, cnew[r], neq, ne, drj, dsj);
+            float4 cnew;
+            upd_row<D>(row[r], pv[r], rj[r], oj[r], qe, cnew, neq, ne, drj, dsj);
             dr = fmax(dr, drj);
             ds = fmax(ds, dsj);
             sh[r] = dsj;
-            cstage[j] = cnew[r];
+            cstage[j] = cnew;
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -2746,80 +2771,129 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     __shared__ unsigned s_ne[NW];
     __shared__ double s_dr[NW], s_ds[NW];
     __shared__ unsigned s_last;
+    // the shift tree's lanes: L < 1024 holds sh[L] (K <= 1024); the first halving
+    // step (lane t += lane t + 512) runs in this thread's registers.  Kept in LDS
+    // for the publisher, so that nothing of the centre phase stays live in
+    // registers through the lists (a 2-blocks-per-CU residency at 512 blocks)
+    static_assert(CAND_TPB == SHIFT_LANES / 2, "thread t holds tree lanes t and t + 512");
+    __shared__ double s_tree[CAND_TPB];
+    s_tree[tid] = sh[0] + (R > 1 ? sh[R > 1 ? 1 : 0] : 0.0);
     if (lane == 0) { s_neq[wv] = neq; s_ne[wv] = ne; s_dr[wv] = dr; s_ds[wv] = ds; }
     __syncthreads();   // every load of this block has returned (its values are used above)
-    if (tid == 0)   // release: this block's loads of the rows the publisher overwrites precede its arrival
-        s_last = arrive_last(ctrl) ? 1u : 0u;
-    unsigned long long changed = 0ull, n_empty = 0ull;
-    double dmax = 0.0, smax = 0.0;
-    for (int w = 0; w < NW; ++w) {
-        changed += s_neq[w]; n_empty += s_ne[w]; dmax = fmax(dmax, s_dr[w]); smax = fmax(smax, s_ds[w]);
-    }
+    // The arrival: issued now, its returned place read after this block's lists.
+    // One same-address atomic per block (512 of them serialise at the memory
+    // side, ~12 ns each): waiting for it here held every block's lists for its
+    // place in that queue ("centres + arrival" 6.2 us of a ~17 us block at
+    // config 3, rd5_updlists_phases_c3.txt).  No release fence: the rows, prev,
+    // C and control words the publisher overwrites were consumed above, and the
+    // lists read only the LDS centres.  The publisher is the last block to
+    // ARRIVE (here), not the last to finish its lists, so its extra work lands
+    // on a block of ordinary length.
+    const unsigned tk = arrive_issue(&ctrl->u_arrive, (unsigned long long)__builtin_amdgcn_readfirstlane(wv == 0 ? 1 : 0));
     // the decisions of upd_publish, identical in every block (same data, order-free maxima)
-    const double slack = 1.0 + 9.094947017729282e-13;
-    const bool rebuild = !(sqrt(dmax) * slack <= budget);
-    double dl_new = alpha * sqrt(smax) * slack;
-    if (!(dl_new <= dl_cap)) dl_new = 0.0;
-    __syncthreads();   // s_last
-    DBG_T(15);
-    if (s_last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        // ---- the publisher: every other block's loads have returned
-        unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
+    auto decide = [&](unsigned long long &n_empty, double &dmax, double &smax, bool &rebuild, double &dl_new) {
+        n_empty = 0ull; dmax = 0.0; smax = 0.0;
+        for (int w = 0; w < NW; ++w) {
+            n_empty += s_ne[w]; dmax = fmax(dmax, s_dr[w]); smax = fmax(smax, s_ds[w]);
+        }
+        const double slack = 1.0 + 9.094947017729282e-13;
+        rebuild = !(sqrt(dmax) * slack <= budget);
+        dl_new = alpha * sqrt(smax) * slack;
+        if (!(dl_new <= dl_cap)) dl_new = 0.0;
+    };
+    {
+        unsigned long long n_empty;
+        double dmax, smax, dl_new;
+        bool rebuild;
+        decide(n_empty, dmax, smax, rebuild, dl_new);
+        // this block's share of the writes nobody reads in this launch: the
+        // relocation snapshot `held` and, on a rebuild, the new reference buffer
+        // (the blocks read cref[sel ^ 1] only speculatively, and use cref[sel])
+        const int share = (K + (int)gridDim.x - 1) / (int)gridDim.x;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int j = tid + CAND_TPB * r;
-            if (j < K) {
+            if (j < K && j / share == (int)blockIdx.x) {
                 const size_t o = (size_t)j * (D + 1);
 #pragma unroll
-                for (int a = 0; a <= D; ++a) {
-                    prev[o + a] = row[r][a];
-                    held[o + a] = row[r][a];   // the relocation snapshot, should this iteration halt
-                    pnext[o + a] = 0ull;       // the next accumulation starts from zero
-                }
-                if (n_empty == 0ull) {         // a halted iteration leaves C (the relocation needs it)
-                    C[j] = cnew[r];
-                    if (rebuild) cref[(size_t)(sel ^ 1u) * K + j] = cnew[r];
-                }
+                for (int a = 0; a <= D; ++a) held[o + a] = row[r][a];
+                if (n_empty == 0ull && rebuild) cref[(size_t)(sel ^ 1u) * K + j] = cstage[j];
             }
         }
-        if (tid == 0) {
-            held[n] = 0ull;
-            if (stats_in) stats_in[n] = 0ull;
-            __hip_atomic_store(&ctrl->u_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (n_empty > 0ull) {
-            if (tid == 0) {
-                ctrl->n_empty = (unsigned)n_empty;
-                ctrl->neq_saved = changed;
-                ctrl->lists = 0u;
-                ctrl->halt = 1u;
-            }
-        } else {
-            // tree lane L < 1024 holds sh[L] (K <= 1024); the first halving step
-            // (lane t += lane t + 512) runs in this thread's registers
-            static_assert(CAND_TPB == SHIFT_LANES / 2, "thread t holds tree lanes t and t + 512");
-            __shared__ double s_tree[CAND_TPB];
-            s_tree[tid] = sh[0] + (R > 1 ? sh[R > 1 ? 1 : 0] : 0.0);
-            __syncthreads();
-            for (int h = SHIFT_LANES / 4; h >= 64; h >>= 1) {
-                if (tid < h) s_tree[tid] = s_tree[tid] + s_tree[tid + h];
-                __syncthreads();
-            }
-            if (wv == 0) {
-                double x = s_tree[lane];
-                for (int st = 32; st > 0; st >>= 1) x = x + __shfl_down(x, st);   // lane t: x_t + x_{t+st}
-                if (lane == 0)
-                    upd_publish(ctrl, changed, x, dmax, smax, sel, alpha, dl_cap, hist_changed, hist_shift, it,
-                                max_iter, budget, tol);
-            }
+        DBG_T(15);
+        // a halted iteration (identical decision in every block) builds no lists
+        if (n_empty == 0ull) {
+            DBG_T(14);
+            // this block's cells: rebuilt at the new centres with the new budget, or refreshed
+            if (rebuild) cand_body<D, 4>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new, CoarseL{});
+            else refresh_body<D>(g, cstage, fc_cnt, fc_rec, fc_lab);
         }
     }
-    if (n_empty > 0ull) return;   // halted: the lists stay (resume rebuilds them)
-    DBG_T(14);
-    // this block's cells: rebuilt at the new centres with the new budget, or refreshed
-    if (rebuild) cand_body<D, 4>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new, CoarseL{});
-    else refresh_body<D>(g, cstage, fc_cnt, fc_rec, fc_lab);
+    if (wv == 0) {
+        const unsigned place = arrive_read(tk);
+        if (lane == 0) s_last = place == gridDim.x - 1u;
+    }
+    __syncthreads();   // s_last
+    DBG_T(3);
+    if (!s_last) return;
+    // ---- the publisher: every other block's loads have returned.  It reads the
+    // rows again (L2; nobody has written them): prev := rows, the next
+    // accumulation target := 0 and (unless halted: the relocation needs the old
+    // C) C := the new centres
+    unsigned long long n_empty;
+    double dmax, smax, dl_new;
+    bool rebuild;
+    decide(n_empty, dmax, smax, rebuild, dl_new);
+    const unsigned long long *src = stats_in ? stats_in : partials + (size_t)par * n;
+    unsigned long long *pnext = stats_in ? stats_in : partials + (size_t)(par ^ 1u) * n;
+    unsigned long long v[R][D + 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int j = tid + CAND_TPB * r;
+        const size_t o = (size_t)(j < K ? j : 0) * (D + 1);
+#pragma unroll
+        for (int a = 0; a <= D; ++a) v[r][a] = src[o + a];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int j = tid + CAND_TPB * r;
+        if (j < K) {
+            const size_t o = (size_t)j * (D + 1);
+#pragma unroll
+            for (int a = 0; a <= D; ++a) prev[o + a] = v[r][a];
+#pragma unroll
+            for (int a = 0; a <= D; ++a) pnext[o + a] = 0ull;   // the next accumulation starts from zero
+            if (n_empty == 0ull) C[j] = cstage[j];
+        }
+    }
+    unsigned long long changed = 0ull;
+    for (int w = 0; w < NW; ++w) changed += s_neq[w];
+    if (tid == 0) {
+        held[n] = 0ull;
+        if (stats_in) stats_in[n] = 0ull;
+        __hip_atomic_store(&ctrl->u_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (n_empty > 0ull) {
+        if (tid == 0) {
+            ctrl->n_empty = (unsigned)n_empty;
+            ctrl->neq_saved = changed;
+            ctrl->lists = 0u;
+            ctrl->halt = 1u;
+        }
+    } else {
+        for (int h = SHIFT_LANES / 4; h >= 64; h >>= 1) {
+            if (tid < h) s_tree[tid] = s_tree[tid] + s_tree[tid + h];
+            __syncthreads();
+        }
+        if (wv == 0) {
+            double x = s_tree[lane];
+            for (int st = 32; st > 0; st >>= 1) x = x + __shfl_down(x, st);   // lane t: x_t + x_{t+st}
+            if (lane == 0)
+                upd_publish(ctrl, changed, x, dmax, smax, sel, alpha, dl_cap, hist_changed, hist_shift, it,
+                            max_iter, budget, tol);
+        }
+    }
+    DBG_T(6);
 }
 
 // ------------------------------------------------------------------ relocation
