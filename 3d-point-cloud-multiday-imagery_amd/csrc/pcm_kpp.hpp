@@ -34,6 +34,10 @@
 namespace pcm {
 
 constexpr int KPP_LMAX = 16;
+#ifndef PCM_KPP_PPL
+#define PCM_KPP_PPL 8
+#endif
+constexpr int KPP_PPL = PCM_KPP_PPL;           // points per lane per pass of one-candidate cell visits
 constexpr int KPP_OB_LOG = 12;                 // original-order weight blocks of 4096 rows
 constexpr int KPP_OB = 1 << KPP_OB_LOG;
 constexpr int KPP_CELL_PTS = 256;              // target points per pruning cell
@@ -175,24 +179,27 @@ __device__ __forceinline__ float wave_max_f(float v) {
     return v;
 }
 
-// Visit the points [b, e) of one cell with a wave, 4 points per lane per pass:
-// the coordinate and `closest` loads of the 4 points are all issued before any
-// is used (a cell holds ~KPP_CELL_PTS = 256 points: one pass, one memory
-// latency, instead of four dependent rounds).  f(i, x, closest_i) per point.
-template <int D, typename F>
+// Visit the points [b, e) of one cell with a wave, PPL points per lane per
+// pass: the coordinate and `closest` loads of the PPL points are all issued
+// before any is used (one memory latency per 64 PPL points instead of PPL
+// dependent rounds).  f(i, x, closest_i) per point.  The grid's cells hold ~380
+// points at config 3 (2^18 cells): PPL = 8 visits most of them in one pass
+// (one-candidate items: eval's per-(candidate, cell) items and apply); PPL = 4
+// where registers are scarce (eval's whole-cell walk keeps 16 candidate sums).
+template <int D, int PPL = 4, typename F>
 __device__ __forceinline__ void kpp_cell_points(const float *__restrict__ xs, const float *__restrict__ closest,
                                                 uint32_t b, uint32_t e, int lane, F &&f) {
-    for (uint32_t i0 = b + lane; i0 < e; i0 += 256) {
-        float x[4][D], cl[4];
+    for (uint32_t i0 = b + lane; i0 < e; i0 += 64u * PPL) {
+        float x[PPL][D], cl[PPL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PPL; ++u) {
             const uint32_t i = i0 + 64u * u;
             const uint32_t ii = i < e ? i : i0;
             kpp_point<D>(xs, ii, x[u]);
             cl[u] = closest[ii];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < PPL; ++u)
             if (i0 + 64u * u < e) f(i0 + 64u * u, x[u], cl[u]);
     }
 }
@@ -550,7 +557,7 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
                 const uint32_t b = (uint32_t)__shfl((int)cb, src), e = (uint32_t)__shfl((int)ce, src);
                 const float4 cd = s_cand[lq];
                 unsigned long long v = 0ull;
-                kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t, const float (&x)[D], float cl) {
+                kpp_cell_points<D, KPP_PPL>(xs, closest, b, e, lane, [&](uint32_t, const float (&x)[D], float cl) {
                     const float d = dist_canon<D>(x, cd);
                     if (d < cl) v += kpp_w(cl, s) - kpp_w(d, s);
                 });
@@ -662,7 +669,7 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
             const long long cell = (long long)__shfl((int)celll, src);   // cell ids < 2^31 (kpp grid <= 2^20 cells)
             const uint32_t b = (uint32_t)__shfl((int)cbl, src), e = (uint32_t)__shfl((int)cel, src);
             float mx = 0.f;
-            kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t i, const float (&x)[D], float cl) {
+            kpp_cell_points<D, KPP_PPL>(xs, closest, b, e, lane, [&](uint32_t i, const float (&x)[D], float cl) {
                 const float d = dist_canon<D>(x, best);
                 if (d < cl) {
                     closest[i] = d;
