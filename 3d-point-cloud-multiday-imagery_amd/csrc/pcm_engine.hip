@@ -1710,7 +1710,8 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
                                                                     um + (size_t)(c - 1) * L, L, scale, c, cmax, nc,
                                                                     ctl);
             LAUNCHCHK();
-            k_kpp_eval<D><<<eg, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
+            if (L <= 8) k_kpp_eval<D, 8><<<eg, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
+            else k_kpp_eval<D><<<eg, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
             LAUNCHCHK();
             k_kpp_apply<D><<<eg, 256, 0, s>>>(xs, perm, cell_start, g, closest, crow, cmax, bsum, X, n, L, scale, c,
                                               c + 1 < k ? 1 : 0, (long long *)indices, ctl);

@@ -445,7 +445,9 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
 // candidates on one load of each point; later, one wave per (candidate, cube
 // cell) item.  Per-lane, per-candidate partial sums in registers, one wave
 // reduction and atomic per candidate at the end.
-template <int D>
+// LM: the candidate accumulators kept per lane (8 when n_local_trials <= 8, as
+// sklearn's 2 + int(log(k)) is up to k = 2980; else KPP_LMAX)
+template <int D, int LM = KPP_LMAX>
 __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, const uint32_t *__restrict__ cell_start,
                                                   Grid g, const float *__restrict__ closest,
                                                   const float *__restrict__ cmax, int L, int s, int c,
@@ -480,9 +482,9 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
     const long long wid = (blockIdx.x * (long long)blockDim.x + tid) >> 6;
     const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
     unsigned dbg_cells = 0;
-    unsigned long long dw[KPP_LMAX];
+    unsigned long long dw[LM];
 #pragma unroll
-    for (int q = 0; q < KPP_LMAX; ++q) dw[q] = 0ull;
+    for (int q = 0; q < LM; ++q) dw[q] = 0ull;
     if (total > g.ncells) {
         // this wave's cells wid, wid + nw, ...: one per lane, each lane tests its
         // cell against every candidate (cmax and the bounds of up to 64 cells
@@ -509,10 +511,13 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
                 bits &= bits - 1ull;
                 const unsigned mask = (unsigned)__shfl((int)lmask, src);
                 const uint32_t b = (uint32_t)__shfl((int)cb, src), e = (uint32_t)__shfl((int)ce, src);
+                // the candidates are re-read from LDS per cell: hoisted out of the
+                // cell loop they held 16 x 4 VGPRs for the whole launch
+                asm volatile("" ::: "memory");
                 kpp_cell_points<D>(xs, closest, b, e, lane, [&](uint32_t, const float (&x)[D], float cl) {
                     const unsigned long long wcl = kpp_w(cl, s);
 #pragma unroll
-                    for (int q = 0; q < KPP_LMAX; ++q) {
+                    for (int q = 0; q < LM; ++q) {
                         if (!((mask >> q) & 1u)) continue;
                         const float d = dist_canon<D>(x, s_cand[q]);
                         if (d < cl) dw[q] += wcl - kpp_w(d, s);
@@ -562,7 +567,7 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
                     if (d < cl) v += kpp_w(cl, s) - kpp_w(d, s);
                 });
 #pragma unroll
-                for (int q = 0; q < KPP_LMAX; ++q)
+                for (int q = 0; q < LM; ++q)
                     if (q == lq) dw[q] += v;
                 if (dbg_cells > 0u && k0 == 0) DBG_E(6);
             }
@@ -576,10 +581,10 @@ __global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, 
     // moves per idle wave were a large share of the launch)
     unsigned long long nz = 0ull;
 #pragma unroll
-    for (int q = 0; q < KPP_LMAX; ++q) nz |= dw[q];
+    for (int q = 0; q < LM; ++q) nz |= dw[q];
     if (__ballot(nz != 0ull) != 0ull) {   // wave-uniform
 #pragma unroll
-        for (int q = 0; q < KPP_LMAX; ++q) {
+        for (int q = 0; q < LM; ++q) {
             if (q >= L) break;
             const unsigned long long v = wave_sum_u64(dw[q]);
             if (lane == 0) s_red[wv][q] = v;
