@@ -1702,10 +1702,15 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
         // (tools/kpp_grid_sweep.sh; 1/8: 162.6 ms); re-swept after the round-3
         // atomics fix: 1/4 109.3-110.2, 1/2 113.3, 1/8 123.4 ms (tools/r4j.sh).
         // PCM_KPP_LATE_*: tuning only
-        static const int late_div = [] { const char *v = std::getenv("PCM_KPP_LATE_DIV"); return v ? std::max(1, std::atoi(v)) : 4; }();
+        // round 5 (eval at 86 VGPRs, 5 waves/SIMD): eval keeps the whole grid, apply
+        // 1/4 -- 94.5 ms vs 95.1 (1/2, 1/4), 94.9 (1/2, 1/2), 95.9 (1/1, 1/8)
+        // (tools/rd5q.sh, profiles/rd5_kpp_steps.txt)
+        static const int late_div = [] { const char *v = std::getenv("PCM_KPP_LATE_DIV"); return v ? std::max(1, std::atoi(v)) : 1; }();
+        static const int apply_div = [] { const char *v = std::getenv("PCM_KPP_APPLY_DIV"); return v ? std::max(1, std::atoi(v)) : 4; }();
         static const int late_c = [] { const char *v = std::getenv("PCM_KPP_LATE_C"); return v ? std::atoi(v) : 64; }();
         for (int c = 1; c < k; ++c) {
             const int eg = c >= late_c ? std::max(ncu, pgrid / late_div) : pgrid;
+            const int ag = c >= late_c ? std::max(ncu, pgrid / apply_div) : pgrid;
             k_kpp_search<D><<<L + KPP_RED_BLOCKS, KPP_STPB, 0, s>>>(bsum, nb, crow, X, n,
                                                                     um + (size_t)(c - 1) * L, L, scale, c, cmax, nc,
                                                                     ctl);
@@ -1713,7 +1718,7 @@ int pcm_kmeanspp(const float *X, int64_t n, int d, int k, int n_local_trials, in
             if (L <= 8) k_kpp_eval<D, 8><<<eg, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
             else k_kpp_eval<D><<<eg, 256, 0, s>>>(xs, cell_start, g, closest, cmax, L, scale, c, ctl);
             LAUNCHCHK();
-            k_kpp_apply<D><<<eg, 256, 0, s>>>(xs, perm, cell_start, g, closest, crow, cmax, bsum, X, n, L, scale, c,
+            k_kpp_apply<D><<<ag, 256, 0, s>>>(xs, perm, cell_start, g, closest, crow, cmax, bsum, X, n, L, scale, c,
                                               c + 1 < k ? 1 : 0, (long long *)indices, ctl);
             LAUNCHCHK();
         }
