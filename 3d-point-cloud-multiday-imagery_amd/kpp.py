@@ -77,11 +77,14 @@ def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_lo
     L = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
     u0 = rs.random_sample()
     umant = np.zeros(max(1, (k - 1) * L), np.uint64)
-    for c in range(1, k):
-        u = rs.uniform(size=L)
+    if k > 1:
+        # sklearn draws uniform(size=L) once per centre (_kmeans.py:239); one draw of
+        # (k - 1) * L doubles is the same stream in the same order (round 5: the
+        # per-centre Python loop cost ~10 ms of host time per call at k = 1024)
+        u = rs.uniform(size=(k - 1) * L)
         m = np.ldexp(u, 53)
         assert np.array_equal(np.ldexp(m, -53), u)      # random_sample doubles are multiples of 2**-53
-        umant[(c - 1) * L:c * L] = m.astype(np.uint64)
+        umant[:] = m.astype(np.uint64)
     if weight_dtype is None:
         weight_dtype = np.float64 if X.dtype == torch.float64 else np.float32
     first = _first_index(n, u0, weight_dtype)

@@ -628,12 +628,20 @@ def main():
             del res
         fit["pt_iters_per_s"] = N * args.fit_iters / (fit["warm_ms"] * 1e-3)
         del eng2
+    kpp_cold_ms = None
     if args.fit and world == 1:
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        pcm_amd.kmeans_plusplus(X, K, random_state=0)
-        torch.cuda.synchronize()
-        kpp_ms = (time.perf_counter() - t0) * 1e3
+        # twice: the first call of the process allocates the workspace (torch's
+        # caching allocator keeps it); the reference's call site seeds n_init=10
+        # times (core.py:227-228), so the second call is the steady cost
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pcm_amd.kmeans_plusplus(X, K, random_state=0)
+            torch.cuda.synchronize()
+            if rep == 0:
+                kpp_cold_ms = (time.perf_counter() - t0) * 1e3
+            else:
+                kpp_ms = (time.perf_counter() - t0) * 1e3
 
     if rank == 0:
         n_local = int(eng.n)      # points this rank's engine holds (its slab at N > 1)
@@ -706,6 +714,7 @@ def main():
             out["stereo_gathers"] = stereo_bench()
         if kpp_ms is not None:
             out["kmeanspp_ms"] = kpp_ms   # GPU k-means++ seeding of the same cloud (K centres), host prep included
+            out["kmeanspp_cold_ms"] = kpp_cold_ms   # the process's first call (workspace allocation)
         if not args.no_cpu and world == 1:
             Xh, Ch = X.float().cpu().numpy(), C0.cpu().numpy()
             if args.config == 2:
