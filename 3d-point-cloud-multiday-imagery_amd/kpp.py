@@ -59,6 +59,22 @@ def _first_index(n: int, u0: float, weight_dtype=np.float32) -> int:
     return min(i, n - 1)
 
 
+def _draws(rs: np.random.RandomState, k: int, L: int):
+    """The random numbers _kmeans_plusplus consumes (sklearn/cluster/_kmeans.py:215-248):
+    the first centre's random_sample() and, per later centre, uniform(size=L) --
+    as their 53-bit mantissas.  One draw of (k - 1) * L doubles is the same stream
+    in the same order (round 5: the per-centre Python loop cost ~4 ms per call
+    at k = 1024; tests/test_kpp.py checks the equality)."""
+    u0 = rs.random_sample()
+    umant = np.zeros(max(1, (k - 1) * L), np.uint64)
+    if k > 1:
+        u = rs.uniform(size=(k - 1) * L)
+        m = np.ldexp(u, 53)
+        assert np.array_equal(np.ldexp(m, -53), u)      # random_sample doubles are multiples of 2**-53
+        umant[:] = m.astype(np.uint64)
+    return u0, umant
+
+
 def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_local_trials=None,
                     weight_dtype=None):
     """GPU k-means++ of a (n, d) cloud on a HIP device; returns (centers (k, d) float32, indices int64).
@@ -75,16 +91,7 @@ def kmeans_plusplus(X: torch.Tensor, n_clusters: int, *, random_state=None, n_lo
         raise ValueError(f"n_samples={n} should be >= n_clusters={k}")
     rs = random_state if isinstance(random_state, np.random.RandomState) else np.random.RandomState(random_state)
     L = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
-    u0 = rs.random_sample()
-    umant = np.zeros(max(1, (k - 1) * L), np.uint64)
-    if k > 1:
-        # sklearn draws uniform(size=L) once per centre (_kmeans.py:239); one draw of
-        # (k - 1) * L doubles is the same stream in the same order (round 5: the
-        # per-centre Python loop cost ~10 ms of host time per call at k = 1024)
-        u = rs.uniform(size=(k - 1) * L)
-        m = np.ldexp(u, 53)
-        assert np.array_equal(np.ldexp(m, -53), u)      # random_sample doubles are multiples of 2**-53
-        umant[:] = m.astype(np.uint64)
+    u0, umant = _draws(rs, k, L)
     if weight_dtype is None:
         weight_dtype = np.float64 if X.dtype == torch.float64 else np.float32
     first = _first_index(n, u0, weight_dtype)

@@ -48,6 +48,18 @@ def test_host_helpers_match_oracle():
             assert K._first_index(n, u) == P.first_index(n, u), (n, u)
 
 
+def test_host_draws_are_sklearns_stream():
+    """kpp._draws (one uniform draw of (k-1)*L doubles) equals the per-centre
+    uniform(size=L) draws _kmeans_plusplus makes (sklearn/cluster/_kmeans.py:239)."""
+    from pcm_amd import kpp as K
+    for seed, k, L in [(0, 1024, 8), (42, 5, 3), (7, 1, 2), (123, 2, 16)]:
+        u0, um = K._draws(np.random.RandomState(seed), k, L)
+        rs = np.random.RandomState(seed)
+        assert u0 == rs.random_sample()
+        ref = [np.ldexp(rs.uniform(size=L), 53).astype(np.uint64) for _ in range(1, k)]
+        np.testing.assert_array_equal(um[:(k - 1) * L], np.concatenate(ref) if ref else np.zeros(0, np.uint64))
+
+
 def test_weights_cannot_overflow():
     X = R.splitmix_uniform(50000, 3, seed=1) * np.float32(1e6)
     s = P.kpp_scale(len(X), P.max_dist_bound(X))
