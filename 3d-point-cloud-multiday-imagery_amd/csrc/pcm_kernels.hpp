@@ -1605,11 +1605,15 @@ constexpr int MASK_MIN = PCM_MASK_MIN;   // sub-cell masks for lists of at least
 constexpr int ZPF = PCM_ZPF;
 template <typename T, int D, int LS, bool MASK>
 constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? (ZPF > 2 ? 5 : 6) : PCM_WPE; }
+// the crowded-layout instance (tile lists, LDS-chunked long lists) does not fit
+// the 6-wave budget: 80 VGPRs spilled 6 to scratch (round 5), so it keeps 5
+template <typename T, int D, int LS, bool MASK, bool CROWD>
+constexpr int lloyd1_wpe_c() { return CROWD ? (lloyd1_wpe<T, D, LS, MASK>() > 5 ? 5 : lloyd1_wpe<T, D, LS, MASK>()) : lloyd1_wpe<T, D, LS, MASK>(); }
 
 // CROWD: the crowded-layout instance (tile lists, long lists, AccL::gwords of
 // dynamic LDS); the other instances compile without that code.
 template <typename T, int D, int LS, bool MASK, bool CROWD = false>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe<T, D, LS, MASK>(), 8))) void k_lloyd1(
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe_c<T, D, LS, MASK, CROWD>(), 8))) void k_lloyd1(
     LloydArgs A, const uint4 *__restrict__ tiles, const float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
     const float4 *__restrict__ Call, const uint32_t *__restrict__ fc_cnt, const float4 *__restrict__ tl_rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t acc[];   // [(LS+1)*(D+1)][AW]
