@@ -1630,7 +1630,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe_
     // or global atomics (12 / 16 slots, rare positions), AccL::gwords when
     // crowded.  Points mostly pick a candidate near their tile, so the lane
     // slots take nearly all of them whatever the list's length.
-    constexpr bool kOvf = !CROWD && (D >= 4 || LS <= 8);
+    // (D <= 3, 8 slots: lists past 8 are rare on the fine grids that take 8
+    // slots, so their overflow goes to global atomics; dropping the 2 KB of LDS
+    // words, 13.0 -> 10.9 KB per block, gave config 3's assign 203.6-204.3 ->
+    // 199.3-199.6 us on one box, round 5, profiles/rd5_lds_ovf_ab.txt)
+    constexpr bool kOvf = !CROWD && D >= 4;
     __shared__ unsigned long long ovf[kOvf ? CAPF * (D + 1) : 1];
     __shared__ uint16_t smap[LCAP];
     __shared__ float skey[LCAP];
