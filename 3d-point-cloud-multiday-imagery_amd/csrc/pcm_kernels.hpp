@@ -1577,6 +1577,9 @@ __device__ __forceinline__ void scan4_s(const float4 *__restrict__ C, int mm, co
 #ifndef PCM_WPE
 #define PCM_WPE 4
 #endif
+#ifndef PCM_WPE_FINE
+#define PCM_WPE_FINE 7
+#endif
 // One Lloyd iteration's E-step + accumulation, ONE TILE PER BLOCK (the round-1
 // persistent tile walk, removed in round 5, measured 211 vs 238 us at config 3).
 // The block's start-up: the tile record, the candidate count and the first
@@ -1597,16 +1600,20 @@ constexpr int MASK_MIN = PCM_MASK_MIN;   // sub-cell masks for lists of at least
 // on one box, tools/wpe_sweep.sh -- across boxes the rocprof average moved
 // only 212.5 -> 211.3 us: the kernel is memory-bound, residency was not the
 // limit); the masked 16-slot variant spills at 6 (12.5M shard
-// 42.0 -> 45.5 us) and D = 4 gains nothing, so they keep 4.
+// 42.0 -> 45.5 us) and D = 4 gains nothing, so they keep 4.  Round 5: once the
+// D <= 3 overflow words left LDS (10.9 KB per block), the fine-grid variant at
+// 7 waves (71 VGPRs, 94 SGPRs; 4 VGPRs spilled outside the rounds) measured
+// 198.3-199.0 -> 195.0-196.3 us per launch at config 3 (events, one box,
+// profiles/rd5_wpe7_ab.txt), so PCM_WPE_FINE is 7.
 // Work items of a compressed tile in flight while one is computed (raw tiles: 2).
 #ifndef PCM_ZPF
 #define PCM_ZPF 2
 #endif
 constexpr int ZPF = PCM_ZPF;
 template <typename T, int D, int LS, bool MASK>
-constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? (ZPF > 2 ? 5 : 6) : PCM_WPE; }
+constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? (ZPF > 2 ? 5 : PCM_WPE_FINE) : PCM_WPE; }
 // the crowded-layout instance (tile lists, LDS-chunked long lists) does not fit
-// the 6-wave budget: 80 VGPRs spilled 6 to scratch (round 5), so it keeps 5
+// a 6-wave budget: 80 VGPRs spilled 6 to scratch (round 5), so it keeps 5
 template <typename T, int D, int LS, bool MASK, bool CROWD>
 constexpr int lloyd1_wpe_c() { return CROWD ? (lloyd1_wpe<T, D, LS, MASK>() > 5 ? 5 : lloyd1_wpe<T, D, LS, MASK>()) : lloyd1_wpe<T, D, LS, MASK>(); }
 
