@@ -1580,6 +1580,12 @@ __device__ __forceinline__ void scan4_s(const float4 *__restrict__ C, int mm, co
 #ifndef PCM_WPE_FINE
 #define PCM_WPE_FINE 7
 #endif
+#ifndef PCM_WPE_D4
+#define PCM_WPE_D4 6
+#endif
+#ifndef PCM_D4_OVF_LDS
+#define PCM_D4_OVF_LDS 0
+#endif
 // One Lloyd iteration's E-step + accumulation, ONE TILE PER BLOCK (the round-1
 // persistent tile walk, removed in round 5, measured 211 vs 238 us at config 3).
 // The block's start-up: the tile record, the candidate count and the first
@@ -1604,14 +1610,21 @@ constexpr int MASK_MIN = PCM_MASK_MIN;   // sub-cell masks for lists of at least
 // D <= 3 overflow words left LDS (10.9 KB per block), the fine-grid variant at
 // 7 waves (71 VGPRs, 94 SGPRs; 4 VGPRs spilled outside the rounds) measured
 // 198.3-199.0 -> 195.0-196.3 us per launch at config 3 (events, one box,
-// profiles/rd5_wpe7_ab.txt), so PCM_WPE_FINE is 7.
+// profiles/rd5_wpe7_ab.txt), so PCM_WPE_FINE is 7.  Likewise the D = 4
+// 8-slot variant without its LDS overflow words (PCM_D4_OVF_LDS 0; positions
+// past the slots go to global atomics) fits 6 waves at 74 VGPRs: config-5
+// 62.5M shard assign 332.7 -> 308.8-312.2 us, 8-way slab ~195 -> ~188 us per
+// rank (profiles/rd5_d4_wpe6_ab.txt), so PCM_WPE_D4 is 6.
 // Work items of a compressed tile in flight while one is computed (raw tiles: 2).
 #ifndef PCM_ZPF
 #define PCM_ZPF 2
 #endif
 constexpr int ZPF = PCM_ZPF;
 template <typename T, int D, int LS, bool MASK>
-constexpr int lloyd1_wpe() { return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? (ZPF > 2 ? 5 : PCM_WPE_FINE) : PCM_WPE; }
+constexpr int lloyd1_wpe() {
+    return (sizeof(T) == 4 && D <= 3 && LS < LSLOT && !MASK) ? (ZPF > 2 ? 5 : PCM_WPE_FINE)
+                                                             : ((D == 4 && LS < LSLOT && !MASK) ? PCM_WPE_D4 : PCM_WPE);
+}
 // the crowded-layout instance (tile lists, LDS-chunked long lists) does not fit
 // a 6-wave budget: 80 VGPRs spilled 6 to scratch (round 5), so it keeps 5
 template <typename T, int D, int LS, bool MASK, bool CROWD>
@@ -1641,7 +1654,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe_
     // slots, so their overflow goes to global atomics; dropping the 2 KB of LDS
     // words, 13.0 -> 10.9 KB per block, gave config 3's assign 203.6-204.3 ->
     // 199.3-199.6 us on one box, round 5, profiles/rd5_lds_ovf_ab.txt)
-    constexpr bool kOvf = !CROWD && D >= 4;
+    constexpr bool kOvf = !CROWD && D >= 4 && PCM_D4_OVF_LDS;
     __shared__ unsigned long long ovf[kOvf ? CAPF * (D + 1) : 1];
     __shared__ uint16_t smap[LCAP];
     __shared__ float skey[LCAP];
