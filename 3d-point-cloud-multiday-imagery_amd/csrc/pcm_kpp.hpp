@@ -447,8 +447,13 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
 // reduction and atomic per candidate at the end.
 // LM: the candidate accumulators kept per lane (8 when n_local_trials <= 8, as
 // sklearn's 2 + int(log(k)) is up to k = 2980; else KPP_LMAX)
+// eval with 8 candidate sums at 6 waves per SIMD (79 VGPRs, no spill): 91.3-91.5
+// -> 90.6 ms per seeding at config 3 (round 5, profiles/rd5_kpp_steps.txt)
+#ifndef PCM_KPP_EVAL_WPE
+#define PCM_KPP_EVAL_WPE 6
+#endif
 template <int D, int LM = KPP_LMAX>
-__global__ __launch_bounds__(256) void k_kpp_eval(const float *__restrict__ xs, const uint32_t *__restrict__ cell_start,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LM <= 8 ? PCM_KPP_EVAL_WPE : 1, 8))) void k_kpp_eval(const float *__restrict__ xs, const uint32_t *__restrict__ cell_start,
                                                   Grid g, const float *__restrict__ closest,
                                                   const float *__restrict__ cmax, int L, int s, int c,
                                                   KppCtl *__restrict__ ctl) {
