@@ -14,9 +14,10 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 SO_PATH = os.environ.get("PCM_SO") or os.path.join(PKG_DIR, "libpcmkm.so")
-UNITS = [os.path.join(PKG_DIR, "csrc", u) for u in ("pcm_engine.hip", "pcm_dense.hip", "pcm_stereo.hip", "pcm_shard.hip")]
+UNITS = [os.path.join(PKG_DIR, "csrc", u) for u in ("pcm_engine.hip", "pcm_dense.hip", "pcm_stereo.hip", "pcm_shard.hip",
+                                                            "pcm_xchg.hip")]
 SOURCES = UNITS + [os.path.join(PKG_DIR, "csrc", h) for h in ("pcm_kernels.hpp", "pcm_kpp.hpp", "pcm_sort.hpp", "pcm_cloud.hpp",
-                                                              "pcm_common.hpp", "pcm_debug.hpp")] + \
+                                                              "pcm_common.hpp", "pcm_debug.hpp", "pcm_xchg.hpp")] + \
     [os.path.join(REPO_DIR, "include", "pcm_kmeans.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
@@ -34,8 +35,10 @@ EXPORTS = [
     "pcm_photoconsistency", "pcm_lr_consistency",
     "pcm_layout_shard", "pcm_shard_hist", "pcm_shard_partition_workspace", "pcm_shard_partition",
     "pcm_shard_scatter_labels", "pcm_assign_kernel_name", "pcm_layout_stream_bytes", "pcm_engine_reserve",
+    "pcm_xchg_create", "pcm_xchg_destroy", "pcm_xchg_handle", "pcm_xchg_open", "pcm_xchg_link", "pcm_xchg_allreduce",
+    "pcm_xchg_status", "pcm_iter_exchange",
 ]
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lock = threading.Lock()
 _lib = None
@@ -64,10 +67,40 @@ def build(force: bool = False, verbose: bool = False) -> str:
     """Compile ``libpcmkm.so`` for gfx950 with hipcc (works without a GPU)."""
     if not force and not needs_build():
         return SO_PATH
-    cmd = [HIPCC, *HIP_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-o", SO_PATH + ".tmp", *UNITS]
+    # the translation units compile in parallel (-c) into an object cache outside
+    # the tree (a unit is rebuilt when it or a header it includes is newer than
+    # its object), then one link
+    import re
+    from concurrent.futures import ThreadPoolExecutor
+    inc = ["-I", os.path.join(REPO_DIR, "include")]
+    objdir = os.environ.get("PCM_OBJ_DIR") or os.path.join("/tmp", "pcm_build_objs")
+    os.makedirs(objdir, exist_ok=True)
+
+    def deps(path, seen):
+        if path in seen or not os.path.exists(path):
+            return seen
+        seen.add(path)
+        for h in re.findall(r'#include\s+"([^"]+)"', open(path).read()):
+            for d in (os.path.dirname(path), os.path.join(REPO_DIR, "include")):
+                if os.path.exists(os.path.join(d, h)):
+                    deps(os.path.join(d, h), seen)
+                    break
+        return seen
+
+    objs, cmds = [], []
+    for u in UNITS:
+        o = os.path.join(objdir, os.path.basename(u) + ".o")
+        objs.append(o)
+        if force or not os.path.exists(o) or any(os.path.getmtime(d) > os.path.getmtime(o) for d in deps(u, set())):
+            cmds.append([HIPCC, *HIP_FLAGS[:-1], *inc, "-c", u, "-o", o])
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        print("\n".join(" ".join(c) for c in cmds))
+    with ThreadPoolExecutor(max_workers=max(1, min(len(cmds), os.cpu_count() or 1))) as ex:
+        for r in list(ex.map(lambda c: subprocess.run(c, capture_output=not verbose, text=True), cmds)):
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed:\n{' '.join(r.args)}\n{r.stdout or ''}{r.stderr or ''}")
+    link = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", SO_PATH + ".tmp", *objs]
+    subprocess.run(link, check=True)
     os.replace(SO_PATH + ".tmp", SO_PATH)
     return SO_PATH
 
@@ -128,6 +161,14 @@ def _declare(lib):
         "pcm_shard_scatter_labels": ([P, P, I64, I64, P, P], I),
         "pcm_assign_kernel_name": ([P, ctypes.c_char_p, ctypes.c_size_t], I),
         "pcm_layout_stream_bytes": ([P, ctypes.POINTER(D), ctypes.POINTER(I64)], I),
+        "pcm_xchg_create": ([I, I64, I, I, D, ctypes.POINTER(P)], I),
+        "pcm_xchg_destroy": ([P], I),
+        "pcm_xchg_handle": ([P, P], I),
+        "pcm_xchg_open": ([P, I, P], I),
+        "pcm_xchg_link": ([P, I, P], I),
+        "pcm_xchg_allreduce": ([P, P, I, P], I),
+        "pcm_xchg_status": ([P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64), P], I),
+        "pcm_iter_exchange": ([P, P, I, P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

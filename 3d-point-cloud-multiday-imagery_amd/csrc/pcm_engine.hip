@@ -20,6 +20,7 @@
 #include "pcm_cloud.hpp"
 #include "pcm_common.hpp"
 #include "pcm_kmeans.h"
+#include "pcm_xchg.hpp"
 
 using namespace pcm;
 
@@ -1225,6 +1226,15 @@ int pcm_iterate(pcm_engine *e, int n, void *stream) {
         if (int rc = iter_global_impl(e, s, parity, false)) return rc;
     }
     return 0;
+}
+
+// The cross-rank SUM of the statistics by peer-memory writes (pcm_xchg.hip),
+// between pcm_iter_local and pcm_iter_global in place of the RCCL all-reduce;
+// gated by the control block like both of them.
+int pcm_iter_exchange(pcm_engine *e, pcm_xchg *x, int phase, void *stream) {
+    if (!e || !x) return fail(PCM_E_ARG, "null engine or exchange");
+    if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
+    return pcm_xchg_launch(x, e->stats, &e->ctrl->halt, phase, (hipStream_t)stream);
 }
 
 int pcm_stats_ptr(pcm_engine *e, void **ptr, int64_t *count) {

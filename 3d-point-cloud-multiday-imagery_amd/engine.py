@@ -139,6 +139,11 @@ class Engine:
     def iter_global(self):
         _lib.check(self.lib.pcm_iter_global(self.h, _stream()), "pcm_iter_global")
 
+    def exchange(self, x, phase: int = 3):
+        """The statistics summed over the ranks by the peer exchange ``x``
+        (``pcm_iter_exchange``; xchg.PeerExchange), in place of the all-reduce."""
+        _lib.check(self.lib.pcm_iter_exchange(self.h, x.h, int(phase), _stream()), "pcm_iter_exchange")
+
     def iterate(self, n: int):
         _lib.check(self.lib.pcm_iterate(self.h, int(n), _stream()), "pcm_iterate")
 

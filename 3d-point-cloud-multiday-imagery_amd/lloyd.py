@@ -16,10 +16,11 @@ Restates the control flow of scikit-learn's ``_kmeans_single_lloyd``
 
 Multi-GPU: rank r receives a contiguous row shard; at layout time the shards are
 regrouped into equal-count spatial slabs (one all_to_all of the points; the
-labels travel back after the final E-step).  The only collective per iteration
-is one SUM all-reduce of K*(D+1)+1 int64 (RCCL over xGMI with the ``nccl``
-backend).  Integer statistics make the result bit-identical for any world size
-and any sharding.
+labels travel back after the final E-step).  Per iteration the ranks sum
+K*(D+1)+1 int64 statistics: by the one-sided peer exchange (``xchg.py``: writes
+into the peers' memory over xGMI, no collective) or by one SUM all-reduce
+(RCCL with the ``nccl`` backend).  Integer statistics make the result
+bit-identical for any world size, sharding and exchange.
 """
 from __future__ import annotations
 
@@ -39,7 +40,11 @@ class LloydResult:
     inertia: float                # global
     n_iter: int
     strict: bool                  # converged by label equality
-    changed: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+    # per iteration: how many of the K*(D+1) integer statistic words differ from the
+    # previous iteration's -- NOT sklearn's count of changed labels (the engine never
+    # stores per-point labels while iterating); 0 exactly when no label
+    # changed, which is when sklearn's strict convergence fires (_kmeans.py:717-722)
+    stat_words_changed: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
     shift: np.ndarray = field(default_factory=lambda: np.zeros(0))
     relocations: int = 0
     layout: dict = field(default_factory=dict)
@@ -65,6 +70,7 @@ def _world(group):
     return 1, 0
 
 
+XCHG_FAILED = 4     # pcm_status.done: a peer exchange timed out
 SLAB_BINS = 16384   # slab histogram resolution (pcm_shard_hist's LDS bound)
 SLAB_MAXP = 16      # PCM_SHARD_MAXP: ranks a slab partition can address (uint8 owner table, LDS counters)
 
@@ -188,14 +194,14 @@ def prepare(engine, X, group=None, shard: str = "auto"):
     return q, n_total
 
 
-def _uses_graph(graph, world, group, split):
-    """HIP-graph replay of the multi-GPU iteration sequence: on by default with
-    RCCL, whose collectives can be captured (gloo's cannot); ``graph=False`` or
-    ``PCM_LLOYD_GRAPH=0`` launches eagerly.  Round 5 made it the default: the
-    captured sequence (k_lloyd1, all-reduce, update) is what ``bench.py --gpus N``
-    measures, a refused capture falls back to eager launches on every rank
-    (``agree``), and the eager sequence pays a host round trip per chunk plus
-    the launch gaps around every collective (``profiles/rd5_split_graph_vs_eager.txt``)."""
+def _uses_graph(graph, world, group, split, xchg=None):
+    """HIP-graph replay of the multi-GPU iteration sequence, on by default:
+    with the peer exchange (``xchg``) the sequence holds no collective, so any
+    backend can capture it; otherwise only RCCL's collectives can be captured
+    (gloo's cannot).  ``graph=False`` or ``PCM_LLOYD_GRAPH=0`` launches eagerly.
+    A refused capture falls back to eager launches on every rank (``agree``);
+    the eager sequence pays a host round trip per chunk plus the launch gaps
+    around every collective (``profiles/rd5_split_graph_vs_eager.txt``)."""
     import os
 
     import torch.distributed as dist
@@ -203,6 +209,8 @@ def _uses_graph(graph, world, group, split):
         graph = os.environ.get("PCM_LLOYD_GRAPH", "1") != "0"
     if not graph or not (world > 1 or split) or not dist.is_initialized():
         return False
+    if xchg is not None:
+        return True
     try:
         return dist.get_backend(group) == "nccl"
     except Exception:   # noqa: BLE001
@@ -221,8 +229,12 @@ def agree(ok: bool, world: int, group=None, device=None) -> bool:
     return bool(int(t.item()))
 
 
-def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, graph=None):
+def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, graph=None, xchg=None):
     """Iteration phase on a prepared engine.  Returns (status, relocations).
+
+    ``xchg``: a verified ``xchg.PeerExchange`` of this rank (world > 1), which
+    sums the statistics over the ranks by peer-memory writes in place of
+    ``dist.all_reduce`` (the sequence then holds no collective).
 
     One process: ``pcm_iterate`` (k_lloyd + fused k_step per iteration).  Several
     (or ``split``): ``iter_local`` (k_lloyd accumulating into the statistics
@@ -237,13 +249,15 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, gra
     engine.begin(C0, tol, max_iter)
     relocs = 0
     it = 0
-    use_graph = _uses_graph(graph, world, group, split)
+    use_graph = _uses_graph(graph, world, group, split, xchg)
     captured = None
 
     def seq(n):
         for _ in range(n):
             engine.iter_local()
-            if world > 1:
+            if xchg is not None:
+                engine.exchange(xchg)
+            elif world > 1:
                 dist.all_reduce(engine.stats, group=group)
             engine.iter_global()
 
@@ -271,6 +285,10 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, gra
         else:
             seq(n_enq)
         st = engine.status()
+        if st["done"] == XCHG_FAILED:
+            from ._lib import PcmError
+            raise PcmError("pcm_amd.lloyd: the peer statistics exchange timed out (a rank stopped pushing); "
+                           "the fit is void")
         if st["halt"]:
             recs = engine.reloc_candidates(int(st["n_empty"]))
             if world > 1:
@@ -308,8 +326,27 @@ def finish(engine, group=None):
     return labels, engine.centers(), inertia
 
 
+def exchange_for(engine, mode: str, group=None):
+    """The statistics exchange of a multi-rank fit (``xchg.choose``), kept on the
+    engine so that later fits reuse it (its setup maps the peers' buffers and
+    runs a self-test).  None: the process-group all-reduce."""
+    world, rank = _world(group)
+    if world <= 1 or mode == "collective" or not getattr(engine, "h", None):
+        return None
+    key = (mode, world, rank, id(group))
+    cached = getattr(engine, "_xchg", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    from . import xchg
+    cnt = engine.stats.numel()
+    x = xchg.choose(mode, cnt, world, group, engine.stats_device)
+    engine._xchg = (key, x)
+    return x
+
+
 def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=None, chunk: int = 8,
-              engine=None, split: bool = False, graph=None, shard: str = "auto") -> LloydResult:
+              engine=None, split: bool = False, graph=None, shard: str = "auto",
+              exchange: str = "auto") -> LloydResult:
     """Fit K-means (Lloyd) to this rank's shard ``X`` (N_local, D) from ``centers_init`` (K, D).
 
     ``tol`` is the absolute centre-shift tolerance (sklearn's ``_tolerance``
@@ -322,14 +359,16 @@ def lloyd_fit(X, centers_init, max_iter: int = 300, tol: float = 0.0, *, group=N
         from .engine import Engine
         engine = Engine(X.shape[1], centers_init.shape[0], X.dtype, max_iter=max_iter)
     prepare(engine, X, group, shard)
-    st, relocs = run(engine, centers_init, max_iter, tol, group, chunk, split, graph)
+    x = exchange_for(engine, exchange, group)
+    st, relocs = run(engine, centers_init, max_iter, tol, group, chunk, split, graph, x)
     labels, centers, inertia = finish(engine, group)
     ch, sh = engine.history(int(st["iter"]))
     layout = engine.layout_info()
     sl = getattr(engine, "_slab", None)
     layout["shard"] = "slab" if sl is not None else "rows"
+    layout["exchange"] = ("peer" if x is not None else "collective") if _world(group)[0] > 1 else None
     if sl is not None:
         layout["slab_points"] = sl["n_slab"]
         layout["slab_axis"] = sl["axis"]
     return LloydResult(labels=labels, centers=centers, inertia=inertia, n_iter=int(st["iter"]),
-                       strict=st["done"] == 1, changed=ch, shift=sh, relocations=relocs, layout=layout)
+                       strict=st["done"] == 1, stat_words_changed=ch, shift=sh, relocations=relocs, layout=layout)

@@ -308,22 +308,35 @@ def slab_proxy(args) -> dict:
     ev = [[[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(P)] for _ in range(args.steps)]
     t_assign = np.zeros(P)
     t_step = np.zeros(P)
+    peer = args.exchange != "collective"
+    xs = None
+    if peer:
+        # the peer exchange between the P engines (linked receive buffers of one
+        # process): each "rank" pushes after its assign and waits + sums before its
+        # update, so both halves of the exchange are inside its timed spans
+        from pcm_amd import xchg
+        xs = xchg.linked(engines[0].stats.numel(), P)
 
     def step(evs):
         for r, e in enumerate(engines):
             if evs:
                 evs[r][0].record()
             e.iter_local()
+            if peer:
+                e.exchange(xs[r], 1)
             if evs:
                 evs[r][1].record()
-        total = engines[0].stats.clone()
-        for e in engines[1:]:
-            total += e.stats
-        for e in engines:
-            e.stats.copy_(total)
+        if not peer:
+            total = engines[0].stats.clone()
+            for e in engines[1:]:
+                total += e.stats
+            for e in engines:
+                e.stats.copy_(total)
         for r, e in enumerate(engines):
             if evs:
                 evs[r][2].record()
+            if peer:
+                e.exchange(xs[r], 2)
             e.iter_global()
             if evs:
                 evs[r][3].record()
@@ -355,13 +368,16 @@ def slab_proxy(args) -> dict:
         bitwise = None
     a_ms, s_ms = t_assign / args.steps, t_step / args.steps
     per_rank = (a_ms + s_ms) * 1e3
-    return {"metric": "per-rank Lloyd iteration cost at P GPUs (1-GPU slab proxy, all-reduce excluded)",
+    what = ("peer exchange included: push after the assign, wait + sum before the update, linked buffers of one "
+            "process (the xGMI hop itself not modelled)") if peer else "all-reduce excluded"
+    return {"metric": f"per-rank Lloyd iteration cost at P GPUs (1-GPU slab proxy, {what})",
             "value": float(per_rank.max()), "unit": "us/iter (max over ranks)", "higher_is_better": False,
             "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "slab_of": P,
             "config": {"workload": f"{'config 5' if args.dtype == 'f16' else 'config 4'} split {P} ways: N={N} "
                                    f"K={K} D={D} {args.dtype}, slabs of axis {axis}"},
             "per_rank_us": {"assign": (a_ms * 1e3).round(2).tolist(), "step": (s_ms * 1e3).round(2).tolist(),
                             "total": per_rank.round(2).tolist()},
+            "exchange": "peer (linked)" if peer else "host-summed (all-reduce emulated)",
             "slabs": info, "centres_bitwise_equal_single_engine": bitwise,
             "slab_engines_agree": bool(ok)}
 
@@ -398,6 +414,11 @@ def main():
                     help="1-GPU proxy of config 4 at P GPUs: the P slab engines of lloyd.prepare's split run on this "
                          "GPU, their statistics summed between the kernels (the all-reduce, emulated); per-rank "
                          "k_lloyd1 + k_step times from HIP events (the per-rank iteration cost, RCCL excluded)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "peer", "collective"],
+                    help="N > 1: how the ranks sum the statistics every iteration -- peer (one-sided writes into the "
+                         "peers' memory, pcm_amd/xchg.py), collective (torch.distributed all_reduce: RCCL) or auto "
+                         "(peer when its setup and self-test pass on every rank); --slab-of P: peer (default) or "
+                         "collective (the statistics summed by torch between the kernels)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "f16"],
                     help="point dtype (f16: config 5's storage; the arithmetic stays canonical fp32)")
     ap.add_argument("--clustered", type=int, default=0, metavar="C",
@@ -456,7 +477,7 @@ def main():
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", world_size=1, rank=0,
                                 device_id=torch.device("cuda", dev_index))
     multi = world > 1 or args.split
-    if world > 1 and args.backend == "gloo":
+    if world > 1 and args.backend == "gloo" and args.exchange == "collective":
         args.graph = False          # gloo collectives cannot be captured
 
     import pcm_amd
@@ -499,6 +520,10 @@ def main():
     lloyd.prepare(eng, X, group, args.shard)
     torch.cuda.synchronize()
     layout_ms = (time.perf_counter() - t0) * 1e3
+    xch = None
+    if world > 1:
+        # the per-iteration statistics sum: the peer exchange (verified on every rank) or the collective
+        xch = lloyd.exchange_for(eng, args.exchange)
     eng.begin(C0, 0.0, max_iter)
 
     ar_events = []
@@ -509,10 +534,13 @@ def main():
         else:
             for _ in range(n):
                 eng.iter_local()
-                if record:   # HIP events around the collective on the launch stream (RCCL's stream joins it)
+                if record:   # HIP events around the exchange on the launch stream (RCCL's stream joins it)
                     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     ev[0].record()
-                dist.all_reduce(eng.stats)
+                if xch is not None:
+                    eng.exchange(xch)
+                else:
+                    dist.all_reduce(eng.stats)
                 if record:
                     ev[1].record()
                     ar_events.append(ev)
@@ -685,6 +713,8 @@ def main():
                        "parallelism": f"dp{world} ({'spatial slabs' if args.shard == 'slab' else 'row shards'})"
                                       if world > 1 else "single GPU",
                        "backend": (args.backend if world > 1 else ("nccl (group of 1)" if multi else None)),
+                       "exchange": (("peer (one-sided writes into the peers' memory)" if xch is not None
+                                     else "collective all_reduce") if world > 1 else None),
                        "launch": "hip-graph" if graph is not None else "eager",
                        "cells": info["ncells"], "tiles": info["ntiles"], "grid": info["grid"],
                        "rank0_points": n_local},

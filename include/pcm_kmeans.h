@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PCM_ABI_VERSION 4
+#define PCM_ABI_VERSION 5
 
 enum pcm_dtype { PCM_F32 = 0, PCM_F16 = 1, PCM_F64 = 2 /* dense path only */ };
 
@@ -56,11 +56,13 @@ enum pcm_err {
 /* Device-side iteration status, copied to the host by pcm_read_status. */
 typedef struct pcm_status {
     uint32_t halt;       /* 1: empty clusters need relocation (pcm_reloc_*) */
-    uint32_t done;       /* 0 running, 1 strict label convergence, 2 shift<=tol, 3 max_iter */
+    uint32_t done;       /* 0 running, 1 strict label convergence, 2 shift<=tol, 3 max_iter,
+                            4 a peer exchange timed out (pcm_iter_exchange; the fit is void) */
     uint32_t iter;       /* completed Lloyd iterations */
     uint32_t n_empty;    /* empty clusters seen by the halted iteration */
     double inertia;      /* local inertia of the last pcm_final (= pcm_inertia_value of the fields below) */
-    uint64_t last_changed;
+    uint64_t last_changed;   /* statistic words (of K*(D+1)) that differ from the previous iteration's:
+                                NOT a count of changed labels -- 0 exactly when no label changed */
     double last_shift;
     /* Exact, order-independent inertia: sum over points of trunc(d * 2^scale)
      * (d = canonical fp32 distance to the final centre) as 32-bit limbs
@@ -158,7 +160,8 @@ int pcm_final(pcm_engine *e, void *stream);
 int pcm_labels(pcm_engine *e, int32_t *out, void *stream);
 /* Current centres (device float32[K*D]). */
 int pcm_get_centers(pcm_engine *e, float *out, void *stream);
-/* Per-iteration history (host arrays of length >= iter): changes, shifts. */
+/* Per-iteration history (host arrays of length >= iter): changed statistic words
+ * (as pcm_status.last_changed; 0 exactly when no label changed), shifts. */
 int pcm_history(pcm_engine *e, uint64_t *changed, double *shift, int cap, void *stream);
 /* Synchronise `stream` and copy the device status. */
 int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream);
@@ -237,6 +240,36 @@ int pcm_shard_partition(const void *X, int dtype, int64_t n, int d, int axis, do
                         void *workspace, size_t workspace_bytes, void *stream);
 int pcm_shard_scatter_labels(const int32_t *labels, const uint32_t *rows, int64_t n, int64_t gidx0, int32_t *out,
                              void *stream);
+
+/* ---------------------------------------------------------------- peer exchange
+ * One-sided SUM of the per-iteration statistics over the ranks (SURVEY.md §8e;
+ * no reference counterpart -- the reference is single-process): it replaces the
+ * RCCL all-reduce between pcm_iter_local and pcm_iter_global by writes into the
+ * peers' memory.  Each rank creates one exchange of `words` int64 (pcm_stats_ptr's
+ * count); its receive buffer (2 x P slots + flags, uncached device memory) is made
+ * reachable to the other ranks by pcm_xchg_handle -> pcm_xchg_open (another
+ * process: IPC) or pcm_xchg_link (an exchange of the same process).  Every rank
+ * must run the same sequence of exchanges.
+ *   pcm_xchg_allreduce  buf (device uint64[words]) := SUM over ranks, in place,
+ *                       stream-ordered, no host synchronisation (graph-capturable);
+ *                       phase 1 = push only, 2 = wait + sum only, 3 = both;
+ *   pcm_iter_exchange   the same on the engine's statistics buffer, gated by the
+ *                       engine's device control block like pcm_iter_*; a wait
+ *                       longer than timeout_s sets status done = 4 (exchange
+ *                       failed) and gates the rest of the fit;
+ *   pcm_xchg_status     synchronises `stream`: err (1 = a wait timed out), and
+ *                       the number of exchanges completed. */
+#define PCM_XCHG_MAXP 16
+#define PCM_XCHG_HANDLE_BYTES 64
+typedef struct pcm_xchg pcm_xchg;
+int pcm_xchg_create(int device, int64_t words, int nranks, int rank, double timeout_s, pcm_xchg **out);
+int pcm_xchg_destroy(pcm_xchg *x);
+int pcm_xchg_handle(pcm_xchg *x, void *handle /* PCM_XCHG_HANDLE_BYTES */);
+int pcm_xchg_open(pcm_xchg *x, int peer, const void *handle);
+int pcm_xchg_link(pcm_xchg *x, int peer, pcm_xchg *other);
+int pcm_xchg_allreduce(pcm_xchg *x, uint64_t *buf, int phase, void *stream);
+int pcm_xchg_status(pcm_xchg *x, uint32_t *err, uint64_t *epoch, void *stream);
+int pcm_iter_exchange(pcm_engine *e, pcm_xchg *x, int phase, void *stream);
 
 /* k-means++ seeding, replacing scikit-learn's _kmeans_plusplus
  * (sklearn/cluster/_kmeans.py:174-272; KMeans' default init, :1012-1019; the

@@ -53,6 +53,34 @@ def test_argument_errors_without_device(lib):
     assert lib.pcm_iter_local(None, None) == -1
 
 
+def test_exchange_argument_errors_without_device(lib):
+    """The peer exchange's argument checks run before any device call."""
+    from pcm_amd import _lib
+    h = ctypes.c_void_p()
+    assert lib.pcm_xchg_create(0, 0, 2, 0, 1.0, ctypes.byref(h)) == -1        # no words
+    assert lib.pcm_xchg_create(0, 8, 17, 0, 1.0, ctypes.byref(h)) == -1       # > PCM_XCHG_MAXP ranks
+    assert lib.pcm_xchg_create(0, 8, 2, 2, 1.0, ctypes.byref(h)) == -1        # rank out of range
+    assert lib.pcm_xchg_create(0, 8, 2, 0, 0.0, ctypes.byref(h)) == -1        # no timeout
+    assert "pcm_xchg_create" in _lib.last_error()
+    assert lib.pcm_iter_exchange(None, None, 3, None) == -1
+    assert lib.pcm_xchg_allreduce(None, None, 3, None) == -1
+    assert lib.pcm_xchg_destroy(None) == 0
+
+
+def test_exchange_choice_host_logic():
+    """xchg.choose / lloyd.exchange_for without a device: one rank or the
+    collective mode never builds an exchange; unknown modes are rejected."""
+    from pcm_amd import lloyd, xchg
+    assert xchg.choose("collective", 8, 4, None, None) is None
+    assert xchg.choose("peer", 8, 1, None, None) is None
+    with pytest.raises(ValueError):
+        xchg.choose("rdma", 8, 4, None, None)
+
+    class Stub:
+        stats = None
+    assert lloyd.exchange_for(Stub(), "auto") is None          # world 1 (no process group)
+
+
 def test_no_fp_contraction_in_build_flags():
     from pcm_amd import _lib
     assert "-ffp-contract=off" in _lib.HIP_FLAGS

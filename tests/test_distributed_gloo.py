@@ -61,7 +61,7 @@ def _worker(rank, world, port, X, C0, max_iter, chunk, out_dir, local=False, sha
         dist.destroy_process_group()
         return
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), labels=res.labels.numpy(), centers=res.centers.numpy(),
-             n_iter=res.n_iter, inertia=res.inertia, changed=res.changed, relocs=res.relocations,
+             n_iter=res.n_iter, inertia=res.inertia, changed=res.stat_words_changed, relocs=res.relocations,
              shard=res.layout.get("shard", "rows"), slab_points=res.layout.get("slab_points", -1))
     dist.barrier()
     dist.destroy_process_group()

@@ -42,7 +42,7 @@ def check(res, ref, where):
     bad = np.flatnonzero(lab != ref["labels"])
     assert bad.size == 0, f"{where}: {bad.size} labels differ, first rows {bad[:8]}"
     assert np.array_equal(cen, ref["centers"]), f"{where}: centres differ (max {np.abs(cen - ref['centers']).max()})"
-    np.testing.assert_array_equal(res.changed > 0, np.asarray(ref["changed"], dtype=np.int64) > 0)
+    np.testing.assert_array_equal(res.stat_words_changed > 0, np.asarray(ref["changed"], dtype=np.int64) > 0)
     assert res.inertia == ref["inertia"]      # exact integer inertia: bitwise equal
 
 

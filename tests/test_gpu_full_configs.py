@@ -67,7 +67,7 @@ def _rank(rank, world, port, n, k, d, f16, max_iter, out_dir):
     torch.cuda.synchronize()
     np.save(os.path.join(out_dir, f"lab{rank}.npy"), res.labels.cpu().numpy())
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), centers=res.centers.cpu().numpy(), n_iter=res.n_iter,
-             inertia=res.inertia, changed=res.changed, shard=res.layout["shard"],
+             inertia=res.inertia, changed=res.stat_words_changed, shard=res.layout["shard"],
              slab_points=res.layout.get("slab_points", -1))
     dist.barrier()
     dist.destroy_process_group()
@@ -165,7 +165,7 @@ def test_config3_bench_length_fit_matches_oracle(gpu):
     bad = np.flatnonzero(res.labels.cpu().numpy() != ref["labels"])
     assert bad.size == 0, f"{bad.size} labels differ from the oracle, first rows {bad[:8]}"
     assert np.array_equal(res.centers.cpu().numpy(), ref["centers"])
-    np.testing.assert_array_equal(np.asarray(res.changed) > 0, np.asarray(ref["changed"], np.int64) > 0)
+    np.testing.assert_array_equal(np.asarray(res.stat_words_changed) > 0, np.asarray(ref["changed"], np.int64) > 0)
     assert float(res.inertia) == ref["inertia"]
     q = fixed_q(X.abs().amax(0).double().cpu().numpy())
     stats = torch.zeros(k * (d + 1), dtype=torch.int64, device="cuda")

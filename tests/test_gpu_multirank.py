@@ -32,7 +32,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, X, C0, max_iter, chunk, dtype, out_dir, shard):
+def _worker(rank, world, port, X, C0, max_iter, chunk, dtype, out_dir, shard, exchange):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -42,20 +42,25 @@ def _worker(rank, world, port, X, C0, max_iter, chunk, dtype, out_dir, shard):
     n = X.shape[0]
     a, b = n * rank // world, n * (rank + 1) // world
     Xs = torch.from_numpy(np.ascontiguousarray(X[a:b])).to("cuda", dtype)
-    res = pcm_amd.lloyd_fit(Xs, torch.from_numpy(C0).cuda(), max_iter=max_iter, tol=0.0, chunk=chunk, shard=shard)
+    res = pcm_amd.lloyd_fit(Xs, torch.from_numpy(C0).cuda(), max_iter=max_iter, tol=0.0, chunk=chunk, shard=shard,
+                            exchange=exchange)
     torch.cuda.synchronize()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), labels=res.labels.cpu().numpy(),
-             centers=res.centers.cpu().numpy(), n_iter=res.n_iter, inertia=res.inertia, changed=res.changed,
-             relocs=res.relocations, shard=res.layout["shard"], slab_points=res.layout.get("slab_points", -1))
+             centers=res.centers.cpu().numpy(), n_iter=res.n_iter, inertia=res.inertia, changed=res.stat_words_changed,
+             relocs=res.relocations, shard=res.layout["shard"], slab_points=res.layout.get("slab_points", -1),
+             exchange=str(res.layout["exchange"]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def run_world(X, C0, max_iter, chunk, tmp_path, world=2, dtype=torch.float32, shard="auto"):
+def run_world(X, C0, max_iter, chunk, tmp_path, world=2, dtype=torch.float32, shard="auto", exchange="peer"):
     import torch.multiprocessing as mp
-    mp.spawn(_worker, args=(world, _free_port(), X, C0, max_iter, chunk, dtype, str(tmp_path), shard), nprocs=world,
-             join=True)
-    return [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
+    mp.spawn(_worker, args=(world, _free_port(), X, C0, max_iter, chunk, dtype, str(tmp_path), shard, exchange),
+             nprocs=world, join=True)
+    parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
+    if exchange != "auto":   # the exchange the fit actually used
+        assert all(str(p["exchange"]) == exchange for p in parts)
+    return parts
 
 
 @pytest.fixture(scope="module")
@@ -85,12 +90,17 @@ def compare(parts, res1, ref):
         assert float(p["inertia"]) == ref["inertia"] == res1.inertia   # exact limbs, all-reduced
 
 
-@pytest.mark.parametrize("chunk,shard", [(1, "slab"), (5, "slab"), (5, "rows")])
-def test_two_ranks_hip_engine(pcm, tmp_path, chunk, shard):
+@pytest.mark.parametrize("chunk,shard,exchange", [(1, "slab", "peer"), (5, "slab", "peer"), (5, "rows", "peer"),
+                                                  (1, "slab", "collective"), (5, "rows", "collective")])
+def test_two_ranks_hip_engine(pcm, tmp_path, chunk, shard, exchange):
+    """Both statistics exchanges: the one-sided peer writes (IPC-mapped buffers of
+    two processes sharing the GPU; with chunk 5 the iterations replay from a
+    captured HIP graph, which the peer exchange allows over gloo) and gloo's
+    all-reduce."""
     X = R.splitmix_uniform(300_000, 3, 41)
     C0 = X[R.init_indices(300_000, 256)]
     ref = R.lloyd_fit(X, C0, max_iter=12, fast=True)
-    parts = run_world(X, C0, 12, chunk, tmp_path, shard=shard)
+    parts = run_world(X, C0, 12, chunk, tmp_path, shard=shard, exchange=exchange)
     assert all(str(p["shard"]) == shard for p in parts)
     compare(parts, single(pcm, X, C0, 12), ref)
 
@@ -103,8 +113,8 @@ def test_two_ranks_hip_engine_fp16_d4(pcm, tmp_path):
     compare(parts, single(pcm, X, C0, 8, torch.float16), ref)
 
 
-@pytest.mark.parametrize("shard", ["slab", "rows"])
-def test_two_ranks_hip_relocation_across_shards(pcm, tmp_path, shard):
+@pytest.mark.parametrize("shard,exchange", [("slab", "peer"), ("rows", "peer"), ("slab", "collective")])
+def test_two_ranks_hip_relocation_across_shards(pcm, tmp_path, shard, exchange):
     """Empty clusters whose farthest points sit on different ranks (slabs: the
     relocation tie-break uses the global rows carried by pcm_layout_shard)."""
     X = R.splitmix_uniform(40_000, 3, 43)
@@ -113,7 +123,7 @@ def test_two_ranks_hip_relocation_across_shards(pcm, tmp_path, shard):
     X[25_000] = [2.5, -1.5, 2.0]         # rank 1
     C0 = np.concatenate([X[:20], np.array([[50, 50, 50], [60, 60, 60], [70, 70, 70]], np.float32)])
     ref = R.lloyd_fit(X, C0, max_iter=20, fast=True)
-    parts = run_world(X, C0, 20, 3, tmp_path, shard=shard)
+    parts = run_world(X, C0, 20, 3, tmp_path, shard=shard, exchange=exchange)
     assert int(parts[0]["relocs"]) >= 1 and int(parts[1]["relocs"]) == int(parts[0]["relocs"])
     compare(parts, single(pcm, X, C0, 20), ref)
 

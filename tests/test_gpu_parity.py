@@ -47,7 +47,7 @@ def assert_same(res, ref, where=""):
     assert bad.size == 0, f"{where} {bad.size} labels differ, first rows {bad[:8]}"
     assert np.array_equal(cen, ref["centers"]), f"{where} centres differ: max {np.abs(cen - ref['centers']).max()}"
     # the engine counts changed statistic words, the oracle changed labels: zero together
-    np.testing.assert_array_equal(res.changed > 0, np.asarray(ref["changed"], dtype=np.int64) > 0)
+    np.testing.assert_array_equal(res.stat_words_changed > 0, np.asarray(ref["changed"], dtype=np.int64) > 0)
     assert res.inertia == ref["inertia"]      # exact integer inertia: bitwise equal
 
 
