@@ -7,8 +7,10 @@ host).  Everything else is the multi-GPU path exactly as the driver's 8-GPU
 run takes it: each rank generates its contiguous row shard of the cloud on the
 device (``synth_uniform(start=...)``), ``lloyd.prepare`` regroups the shards
 into spatial slabs (histogram all-reduce, stable partition, ``all_to_all`` of
-the points and their global rows), every iteration all-reduces the integer
-statistics, and the final labels travel back to the row owners.
+the points and their global rows), every iteration sums the integer statistics
+over the ranks by the one-sided peer exchange (round 6: IPC-mapped receive
+buffers of the 8 processes, pcm_amd/xchg.py -- what the driver's 8-GPU run
+takes by default), and the final labels travel back to the row owners.
 
 * config 4: N=100M, K=1024, D=3 fp32, 12.5M rows per rank, 8 iterations (list
   rebuilds and refreshes on the 12.5M slabs, round 5);
@@ -68,6 +70,7 @@ def _rank(rank, world, port, n, k, d, f16, max_iter, out_dir):
     np.save(os.path.join(out_dir, f"lab{rank}.npy"), res.labels.cpu().numpy())
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), centers=res.centers.cpu().numpy(), n_iter=res.n_iter,
              inertia=res.inertia, changed=res.stat_words_changed, shard=res.layout["shard"],
+             exchange=str(res.layout["exchange"]),
              slab_points=res.layout.get("slab_points", -1))
     dist.barrier()
     dist.destroy_process_group()
@@ -111,6 +114,7 @@ def _compare(parts, labels, ref, n):
     assert sum(int(p["slab_points"]) for p in parts) == n
     for p in parts:
         assert str(p["shard"]) == "slab"
+        assert str(p["exchange"]) == "peer"      # the one-sided exchange (IPC over gloo), not the all-reduce
         assert np.array_equal(p["centers"], ref["centers"])
         assert int(p["n_iter"]) == ref["n_iter"]
         np.testing.assert_array_equal(np.asarray(p["changed"]) > 0, np.asarray(ref["changed"], np.int64) > 0)
