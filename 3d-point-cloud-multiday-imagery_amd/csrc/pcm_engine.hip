@@ -738,7 +738,6 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     }
     k_tile_counts<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, nc, tcnt, e->tile_cap);
     LAUNCHCHK();
-    LAUNCHCHK();
     size_t sb = scan_bytes;
     if (rocprim::exclusive_scan(tmp, sb, tcnt, e->tile_off, 0u, (size_t)nc, rocprim::plus<uint32_t>(), s) != hipSuccess)
         return fail(PCM_E_HIP, "layout: tile scan");
@@ -1016,8 +1015,10 @@ static int timing_mark(pcm_engine *e, int which, hipStream_t s) {
 
 // k_lloyd (its candidate lists were built by the previous k_lists, the resume
 // path or pcm_fit_begin).  to_stats: accumulate straight into `stats` (the
-// all-reduce buffer, zeroed by the previous k_upd / k_global / fit_begin);
-// otherwise into the single-GPU parity half partials[iter & 1].
+// statistics buffer every fit iterates through -- one GPU or the all-reduce /
+// peer-exchange buffer of several -- zeroed by the previous update's
+// publisher, k_global or fit_begin); otherwise into partials[iter & 1], which
+// only the assign-timing calibration (pcm_time_assign) still uses.
 static int iter_local_impl(pcm_engine *e, hipStream_t s, bool to_stats) {
     if (int rc = timing_mark(e, 0, s)) return rc;
     if (int rc = launch_tile_lists(e, s, 1)) return rc;   // crowded layouts only
@@ -1062,8 +1063,8 @@ int pcm_iter_local(pcm_engine *e, void *stream) {
     return iter_local_impl(e, (hipStream_t)stream, true);   // into `stats`: the caller all-reduces it
 }
 
-// Centre update + next candidate lists.  stats_in: the all-reduced statistics
-// (multi-GPU) or nullptr (single GPU: partials[parity]).  Every K: k_upd (the
+// Centre update + next candidate lists.  from_partials = false (every fit): the
+// kernels read `stats` (the summed statistics); true: partials[iter & 1].  Every K: k_upd (the
 // K new centres once, convergence, history) then k_lists (C := new centres,
 // this block's lists rebuilt or refreshed).  The relocation resume takes
 // k_global (it handles `resume`) + k_cand.
@@ -1212,18 +1213,17 @@ int pcm_time_assign(pcm_engine *e, int reps, void *stream, double *ms) {
 
 // Single-process iterations: the multi-GPU sequence without the all-reduce --
 // k_lloyd1 into the statistics buffer, then the update reading it in place (its
-// publisher zeroes it once every block has read it).  Round 5: the parity halves
-// of `partials` that the single-GPU path used before made every k_updlists block
-// load both halves (the parity is a device control word): 32 of its 144 B per
-// centroid row, all blocks, from L2.  PCM_PARITY_ITER=1 keeps the old path (A/B).
+// publisher zeroes it once every block has read it).  (Round 5 retired the
+// parity halves of `partials` on this path: they made every k_updlists block
+// load both halves, 32 of its 144 B per centroid row; round 6 removed the A/B
+// switch that kept them.)
 int pcm_iterate(pcm_engine *e, int n, void *stream) {
     if (!e || n < 0) return fail(PCM_E_ARG, "bad argument");
     if (!e->fit_ready) return fail(PCM_E_STATE, "pcm_fit_begin must run first");
     hipStream_t s = (hipStream_t)stream;
-    static const bool parity = [] { const char *v = std::getenv("PCM_PARITY_ITER"); return v && std::atoi(v) == 1; }();
     for (int i = 0; i < n; ++i) {
-        if (int rc = iter_local_impl(e, s, !parity)) return rc;
-        if (int rc = iter_global_impl(e, s, parity, false)) return rc;
+        if (int rc = iter_local_impl(e, s, true)) return rc;
+        if (int rc = iter_global_impl(e, s, false, false)) return rc;
     }
     return 0;
 }

@@ -2867,7 +2867,12 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     // ---- the publisher: every other block's loads have returned.  It reads the
     // rows again (L2; nobody has written them): prev := rows, the next
     // accumulation target := 0 and (unless halted: the relocation needs the old
-    // C) C := the new centres
+    // C) C := the new centres.  Invariant the zeroing relies on: every
+    // block consumed its loads of prev, C and the statistics rows (their values
+    // feed the centres above) before it arrived; a load left in flight at an
+    // arrival is one whose value is discarded -- the `alt` half of `partials`,
+    // issued only when stats_in is null, a path no engine entry takes since
+    // round 6 (pcm_iterate / pcm_iter_global always pass the statistics buffer).
     unsigned long long n_empty;
     double dmax, smax, dl_new;
     bool rebuild;

@@ -92,15 +92,15 @@ __device__ __forceinline__ unsigned long long *slot(const XArgs &a, unsigned lon
 // drained them (vmcnt(0)) and met the others at the barrier, one lane raises the
 // flag -- no release fence (MI355X_MICROARCH.md "Valid forms", producer, the
 // sc1-stores form).  !WT: plain stores + a system release fence (A/B).
-template <bool WT>
-__global__ __launch_bounds__(PUSH_TPB) void k_xpush(const unsigned long long *__restrict__ src, XArgs a) {
+template <bool WT, int TPB, int VEC>
+__device__ __forceinline__ void push_body(const unsigned long long *__restrict__ src, const XArgs &a, int blk) {
     unsigned long long *mine = a.peer[a.rank];
     const int tid = threadIdx.x;
     const long long last = a.W - 1;
-    unsigned long long v[PUSH_VEC];
+    unsigned long long v[VEC];
 #pragma unroll
-    for (int u = 0; u < PUSH_VEC; ++u) {
-        const long long i = (long long)tid + (long long)u * PUSH_TPB;
+    for (int u = 0; u < VEC; ++u) {
+        const long long i = (long long)tid + (long long)u * TPB;
         v[u] = src[i < last ? i : last];
     }
     const unsigned gate = a.gate[0] | a.gate[1];
@@ -108,23 +108,23 @@ __global__ __launch_bounds__(PUSH_TPB) void k_xpush(const unsigned long long *__
     const unsigned long long e = ld_sys(mine + EPOCH_W);
     const bool go = (gate | (unsigned)err) == 0u;
     const unsigned par = (unsigned)(e & 1ull);
-    const int dst = (a.rank + 1 + (int)blockIdx.x) % a.P;
+    const int dst = (a.rank + 1 + blk) % a.P;
     unsigned long long *base = a.peer[dst];
     unsigned long long *out = go ? slot(a, base, par, a.rank) : slot(a, mine, par, a.rank);
     for (long long b = 0;;) {
 #pragma unroll
-        for (int u = 0; u < PUSH_VEC; ++u) {
-            const long long i = b + tid + (long long)u * PUSH_TPB;
+        for (int u = 0; u < VEC; ++u) {
+            const long long i = b + tid + (long long)u * TPB;
             if (i < a.W) {
                 if constexpr (WT) st_sys(out + i, v[u]);
                 else out[i] = v[u];
             }
         }
-        b += (long long)PUSH_VEC * PUSH_TPB;
+        b += (long long)VEC * TPB;
         if (b >= a.W) break;
 #pragma unroll
-        for (int u = 0; u < PUSH_VEC; ++u) {
-            const long long i = b + tid + (long long)u * PUSH_TPB;
+        for (int u = 0; u < VEC; ++u) {
+            const long long i = b + tid + (long long)u * TPB;
             v[u] = src[i < last ? i : last];
         }
     }
@@ -147,14 +147,14 @@ __global__ __launch_bounds__(PUSH_TPB) void k_xpush(const unsigned long long *__
 // barrier.  The slot loads are 8-B system-scope loads of words the producers
 // stored write-through, issued after the barrier that follows the matched poll
 // (the consumer's sc1-loads form: no acquire fence; a.acq = 1 adds one, A/B).
-template <int NP>
-__global__ __launch_bounds__(SUM_TPB) void k_xsum(unsigned long long *__restrict__ buf, XArgs a) {
+template <int NP, int TPB>
+__device__ __forceinline__ void sum_body(unsigned long long *__restrict__ buf, const XArgs &a, int blk, int nblk) {
     __shared__ int s_state;                  // 0 go, 1 gated, 2 timed out
     __shared__ unsigned long long s_e;
     unsigned long long *mine = a.peer[a.rank];
     const int tid = threadIdx.x, lane = tid & 63;
     // the own statistics (the previous kernel's) load while wave 0 polls
-    const long long i0 = ((long long)blockIdx.x * SUM_TPB + tid) * SUM_WORDS;
+    const long long i0 = ((long long)blk * TPB + tid) * SUM_WORDS;
     long long ix[SUM_WORDS];
 #pragma unroll
     for (int w = 0; w < SUM_WORDS; ++w) ix[w] = i0 + w < a.W ? i0 + w : a.W - 1;
@@ -224,11 +224,24 @@ __global__ __launch_bounds__(SUM_TPB) void k_xsum(unsigned long long *__restrict
     if (tid == 0) {
         const unsigned long long old =
             __hip_atomic_fetch_add(mine + ARRIVE_W, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (old == gridDim.x - 1ull) {
+        if (old == (unsigned long long)nblk - 1ull) {
             st_sys(mine + ARRIVE_W, 0ull);
             st_sys(mine + EPOCH_W, e + 1ull);
         }
     }
+}
+
+// Push and sum stay two launches: in one launch the summing blocks would
+// overwrite the statistics while this rank's pushing blocks may still be
+// reading them (a 3-rank self-test caught exactly that, round 6).
+template <bool WT>
+__global__ __launch_bounds__(PUSH_TPB) void k_xpush(const unsigned long long *__restrict__ src, XArgs a) {
+    push_body<WT, PUSH_TPB, PUSH_VEC>(src, a, (int)blockIdx.x);
+}
+
+template <int NP>
+__global__ __launch_bounds__(SUM_TPB) void k_xsum(unsigned long long *__restrict__ buf, XArgs a) {
+    sum_body<NP, SUM_TPB>(buf, a, (int)blockIdx.x, (int)gridDim.x);
 }
 
 }  // namespace pcm_xc

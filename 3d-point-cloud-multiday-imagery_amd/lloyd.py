@@ -195,22 +195,24 @@ def prepare(engine, X, group=None, shard: str = "auto"):
 
 
 def _uses_graph(graph, world, group, split, xchg=None):
-    """HIP-graph replay of the multi-GPU iteration sequence, on by default:
-    with the peer exchange (``xchg``) the sequence holds no collective, so any
-    backend can capture it; otherwise only RCCL's collectives can be captured
-    (gloo's cannot).  ``graph=False`` or ``PCM_LLOYD_GRAPH=0`` launches eagerly.
-    A refused capture falls back to eager launches on every rank (``agree``);
-    the eager sequence pays a host round trip per chunk plus the launch gaps
-    around every collective (``profiles/rd5_split_graph_vs_eager.txt``)."""
+    """HIP-graph replay of the multi-GPU iteration sequence.  With the peer
+    exchange (``xchg``) the sequence holds no collective: captured by default,
+    on any backend (``graph=False`` or ``PCM_LLOYD_GRAPH=0`` launches eagerly).
+    With the collective all-reduce only RCCL's collectives can be captured
+    (gloo's cannot), and since round 6 that capture is opt-in (``graph=True`` or
+    ``PCM_LLOYD_GRAPH=1``): the collective is now the fallback path, and a
+    captured multi-rank RCCL sequence has no multi-GPU run on record.
+    A refused capture falls back to eager launches on every rank (``agree``)."""
     import os
 
     import torch.distributed as dist
-    if graph is None:
-        graph = os.environ.get("PCM_LLOYD_GRAPH", "1") != "0"
-    if not graph or not (world > 1 or split) or not dist.is_initialized():
+    env = os.environ.get("PCM_LLOYD_GRAPH")
+    if not (world > 1 or split) or not dist.is_initialized():
         return False
     if xchg is not None:
-        return True
+        return graph is not False and env != "0"
+    if not (graph is True or (graph is None and env == "1")):
+        return False
     try:
         return dist.get_backend(group) == "nccl"
     except Exception:   # noqa: BLE001
