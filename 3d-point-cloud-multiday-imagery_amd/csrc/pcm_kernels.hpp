@@ -30,7 +30,11 @@ constexpr int MSLOT = 4;           // LDS-privatised slots per lane (nearest-to-
 #define PCM_TPB 128   // 128 measured 9% faster than 256 at 100M (two-wave barriers), 10% at 12.5M
 #endif
 constexpr int TPB = PCM_TPB;       // assign block size
-constexpr int TILE = 32 * TPB;     // max points per tile: <= 32 per lane, 64 per shared LDS word (see AccL)
+#ifndef PCM_TILE_PTS
+#define PCM_TILE_PTS (32 * PCM_TPB)
+#endif
+constexpr int TILE = PCM_TILE_PTS;  // max points per tile: <= 32 per lane, 64 per shared LDS word (see AccL)
+static_assert(TILE <= 64 * (TPB >= 128 ? TPB / 2 : TPB), "an LDS word sums <= 64 points (int32-exact)");
 constexpr uint32_t FULL = 0xFFFFFFFFu;
 constexpr int TLCAP = 256;        // tile lists staged whole in k_lloyd1's LDS (slot-map path)
 constexpr int TLMAX = 1024;       // tile-list capacity (longer lists: FULL); lists past TLCAP scan in LDS chunks
