@@ -624,9 +624,18 @@ def main():
         dt, assign_ms = float(every[:, 0].max()), float(every[:, 1].max())
         per_rank = {"assign": every[:, 1].round(5).tolist(), "update": every[:, 2].round(5).tolist(),
                     "tile_lists": every[:, 3].round(5).tolist(),
-                    "allreduce": every[:, 4].round(5).tolist() if allreduce_ms is not None else None,
+                    "exchange" if xch is not None else "allreduce":
+                        every[:, 4].round(5).tolist() if allreduce_ms is not None else None,
                     "points": every[:, 5].astype(np.int64).tolist(),
                     "wall_ms_per_step": (every[:, 0] * 1e3 / args.steps).round(5).tolist()}
+        # every rank must hold the same centres after the run (they are computed from the
+        # summed statistics): a cheap end-to-end check of the exchange at this world size
+        ch = eng.centers().reshape(-1).view(torch.int32).to(torch.int64)
+        digest = torch.stack([ch.sum(), (ch * torch.arange(1, ch.numel() + 1, device=ch.device)).sum()])
+        digest = digest.to("cuda" if args.backend == "nccl" else "cpu")
+        dg = [torch.zeros_like(digest) for _ in range(world)]
+        dist.all_gather(dg, digest)
+        per_rank["centres_agree"] = bool(all(torch.equal(d, dg[0]) for d in dg))
     else:
         assign_ms = tm["assign_ms"]
     launch_ms, b2b_ms = assign_ms, None
@@ -729,7 +738,8 @@ def main():
                          "compute": compute_roofline(n_local, K, D, cand.get("mean", 0.0), launch_ms)},
             "breakdown_ms_per_iter": {"assign": assign_ms, "update": tm["tail_ms"],
                                       "tile_lists": tm.get("candidates_ms", 0.0),
-                                      **({"allreduce": allreduce_ms} if allreduce_ms is not None else {}),
+                                      **({("exchange" if xch is not None else "allreduce"): allreduce_ms}
+                                         if allreduce_ms is not None else {}),
                                       **({"per_rank": per_rank} if per_rank is not None else {})},
             "candidates": cand,
             "layout_ms": layout_ms,

@@ -1,45 +1,45 @@
-"""Diagnose a linked-exchange mismatch: which words differ, and what they hold."""
-import sys
+"""Replay test_linked_allreduce_exact's sequence with diagnostics on a mismatch."""
 import os
+import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
-import pcm_amd
+import pcm_amd  # noqa: F401
 from pcm_amd import xchg
 
-P, W = int(sys.argv[1]), int(sys.argv[2])
-SYNC = len(sys.argv) > 3 and sys.argv[3] == "sync"
-xs = xchg.linked(W, P)
-g = torch.Generator(device="cuda").manual_seed(7)
-hist = []
-for rnd in range(4):
-    bufs = [torch.randint(-2**40, 2**40, (W,), dtype=torch.int64, device="cuda", generator=g) for _ in range(P)]
-    orig = [b.clone() for b in bufs]
-    want = sum(orig)
-    for r in range(P):
-        xs[r].allreduce(bufs[r], 1)
-    if SYNC:
+def case(P, words, diag):
+    xs = xchg.linked(words, P)
+    g = torch.Generator(device="cuda").manual_seed(P * 1000 + words)
+    prev = None
+    for rnd in range(5):
+        bufs = [torch.randint(-2**62, 2**62, (words,), dtype=torch.int64, device="cuda", generator=g) for _ in range(P)]
+        orig = [b.clone() for b in bufs]
+        want = sum(b.clone() for b in bufs)
+        for r in range(P):
+            xs[r].allreduce(bufs[r], 1)
+        for r in range(P):
+            xs[r].allreduce(bufs[r], 2)
         torch.cuda.synchronize()
-    for r in range(P):
-        xs[r].allreduce(bufs[r], 2)
-    torch.cuda.synchronize()
-    hist.append(orig)
-    for r in range(P):
-        bad = (bufs[r] != want).nonzero().flatten().cpu()
-        if bad.numel():
-            diff = (bufs[r] - want)[bad]
-            # which peers' contributions are missing / stale?
-            expl = []
-            i0 = int(bad[0])
-            for s in range(P):
-                if s == r:
-                    continue
-                cur, prev = orig[s][i0], hist[-2][s][i0] if len(hist) > 1 else None
-                expl.append((s, int(cur), None if prev is None else int(prev)))
-            if len(hist) > 1:
-                stale = orig[r][bad] + sum(hist[-2][s][bad] for s in range(P) if s != r)
-                print("   bad words == own + previous round's peers:", bool(torch.equal(stale, bufs[r][bad])),
-                      " bad blocks (512 words):", sorted(set((bad // 512).tolist())))
-            print(f"rnd {rnd} rank {r}: {bad.numel()} bad words, first {int(bad[0])} last {int(bad[-1])}, "
-                  f"diff at first {int(diff[0])}; peers (cur, prev) at first: {expl}")
-    if SYNC:
-        print("rnd", rnd, "status", [x.status() for x in xs])
+        for r in range(P):
+            if not torch.equal(bufs[r], want):
+                bad = (bufs[r] != want).nonzero().flatten()
+                print(f"P={P} W={words} rnd {rnd} rank {r}: {bad.numel()} bad, blocks {sorted(set((bad // 512).tolist()))[:20]}")
+                if diag and prev is not None:
+                    got = bufs[r][bad]
+                    stale = orig[r][bad] + sum(prev[s][bad] for s in range(P) if s != r)
+                    print("  == own + previous round's peers:", bool(torch.equal(stale, got)))
+                    for s in range(P):
+                        if s == r:
+                            continue
+                        miss = want[bad] - orig[s][bad] + prev[s][bad]
+                        if torch.equal(miss, got):
+                            print("  == sender", s, "stale")
+                    print("  xs status", [x.status() for x in xs])
+                return False
+        prev = orig
+    print(f"P={P} W={words} ok", [x.status()["epoch"] for x in xs])
+    return True
+
+for P, W in [(2, 4097), (3, 1), (3, 4096), (8, 4097), (8, 20481), (16, 257)]:
+    case(P, W, True)
+print("alone:")
+case(8, 20481, True)
