@@ -358,7 +358,7 @@ def slab_proxy(args) -> dict:
     ok = all(np.array_equal(C_slab, e.centers().cpu().numpy()) for e in engines)
     info = [dict(e.layout_info(), points=int(e.n), kernel=e.assign_kernel(), **e.candidate_stats()) for e in engines]
     del engines
-    if N <= ENGINE_MAX_POINTS:
+    if N <= ENGINE_MAX_POINTS and os.environ.get("PCM_PROXY_NOCHECK") != "1":   # (=1: kernel traces of the proxy alone)
         one = Engine(D, K, pdt, max_iter=iters + 4)
         lloyd.prepare(one, X, lloyd.LOCAL)
         one.begin(C0, 0.0, iters + 4)
