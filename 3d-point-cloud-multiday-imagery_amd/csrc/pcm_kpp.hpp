@@ -90,12 +90,11 @@ __device__ __forceinline__ void kpp_point(const float *__restrict__ xs, long lon
 
 // Conservative reach test: true iff some point of the cell may have a
 // canonical fp32 distance to c strictly below cmax (the cell's max closest).
+// The cell is given by its fine coordinates f (its fp64 box computed here) or,
+// for a box tested against several candidates, by the box itself.
 template <int D>
-__device__ __forceinline__ bool kpp_reaches(const Grid &g, long long cell, const float4 &c, float cmax) {
-    int f[MAXD];
-    decode(cell, g.G, D, f);
-    double blo[MAXD], bhi[MAXD];
-    cell_box<D>(g, f, f, blo, bhi);
+__device__ __forceinline__ bool kpp_reaches_box(const double (&blo)[MAXD], const double (&bhi)[MAXD], const float4 &c,
+                                                float cmax) {
     double m = 0.0;
 #pragma unroll
     for (int a = 0; a < D; ++a) {
@@ -105,6 +104,26 @@ __device__ __forceinline__ bool kpp_reaches(const Grid &g, long long cell, const
     }
     // d~ >= d (1 - 5u) - 3 * 2^-150 (DESIGN.md "Exactness of pruning")
     return m * (1.0 - PEPS) - PTAU < (double)cmax;
+}
+
+template <int D>
+__device__ __forceinline__ bool kpp_reaches_f(const Grid &g, const int (&f)[MAXD], const float4 &c, float cmax) {
+    double blo[MAXD], bhi[MAXD];
+    cell_box<D>(g, f, f, blo, bhi);
+    return kpp_reaches_box<D>(blo, bhi, c, cmax);
+}
+
+// fine coordinates of a cell id with 32-bit divisions (the k-means++ grid holds
+// <= 2^20 cells): the 64-bit div/mod of `decode` expand to long sequences, and
+// the late steps run one reach test per lane on their critical path
+template <int D>
+__device__ __forceinline__ void decode32(unsigned c, const int *G, int (&f)[MAXD]) {
+#pragma unroll
+    for (int a = D - 1; a >= 0; --a) {
+        const unsigned gd = (unsigned)G[a];
+        f[a] = (int)(c % gd);
+        c /= gd;
+    }
 }
 
 // Cell-index cube around c of half-width sqrt(gmax) (+ one cell of binning slack).
@@ -128,13 +147,14 @@ __device__ __forceinline__ void kpp_cube(const Grid &g, const float4 &c, float g
     }
 }
 
+// Cube item `local` (< 2^31: a cube never exceeds the grid) -> its fine
+// coordinates f and cell id, 32-bit divisions.
 template <int D>
 __device__ __forceinline__ long long kpp_cube_cell(const Grid &g, const int (&i0)[MAXD], const int (&i1)[MAXD],
-                                                   long long local) {
-    int f[MAXD];
+                                                   unsigned local, int (&f)[MAXD]) {
 #pragma unroll
     for (int a = D - 1; a >= 0; --a) {
-        const int w = i1[a] - i0[a] + 1;
+        const unsigned w = (unsigned)(i1[a] - i0[a] + 1);
         f[a] = i0[a] + (int)(local % w);
         local /= w;
     }
@@ -167,6 +187,13 @@ __device__ __forceinline__ unsigned long long wave_scan_u64(unsigned long long v
 __device__ __forceinline__ unsigned long long wave_last_u64(unsigned long long v) {
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// lane `src`'s value (uniform src), broadcast
+__device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long v, int src) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), src);
     return ((unsigned long long)hi << 32) | lo;
 }
 
@@ -332,6 +359,7 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
     if (t == 0)
         for (int l = tid; l < KPP_DREP * KPP_LMAX; l += KPP_STPB) (&ctl->drep[0][0])[l] = 0ull;
     __shared__ unsigned long long wtot[NWV];
+    __shared__ unsigned long long s_tr[KPP_SCU][64];   // the target wave's chunks, transposed (16 KB)
     __shared__ long long s_blk;
     __shared__ unsigned long long s_res;
     __shared__ long long s_found;
@@ -367,23 +395,39 @@ __global__ __launch_bounds__(KPP_STPB) void k_kpp_search(const unsigned long lon
     for (int w = 0; w < wv; ++w) base += wtot[w];
     const bool mine = (tg == 0ull) ? (sb == 0 && se > 0) : (base < tg && tg <= base + wsum);
     if (mine) {   // wave-uniform
-        // the chunk holding the target from the chunk totals (register chunks:
-        // static indices), then one wave prefix scan of that chunk
+        // the chunk holding the target: the wave's register cache transposed
+        // through LDS, lane u < CU sums chunk u (one 8-B read per lane and step,
+        // rotated so that the 32 lanes hit distinct banks), one wave scan over the
+        // chunk totals; then one wave scan of that chunk (round 6: 32 dependent
+        // wave scans of the chunks in registers took 3.6 us of the launch's 10.6,
+        // tools/kpp_timing.py)
+#pragma unroll
+        for (int u = 0; u < CU; ++u) s_tr[u][lane] = v[u];
+        unsigned long long ct = 0ull;
+        if (lane < CU) {
+#pragma unroll 16
+            for (int j = 0; j < 64; ++j) ct += s_tr[lane][(j + lane) & 63];
+        }
+        const unsigned long long ci = wave_scan_u64(ct);   // inclusive over the chunks (lanes >= CU add 0)
+        const bool hit = lane < CU && lane < nch && base + ci >= tg;
+        const unsigned long long hb = __ballot(hit);
         unsigned long long r = base, x = 0ull, xi = 0ull;
         int uc = -1;
-#pragma unroll
-        for (int u = 0; u < CU; ++u) {
-            const unsigned long long inc = wave_scan_u64(v[u]);   // independent scans: VALU ILP
-            const unsigned long long ct = wave_last_u64(inc);
-            if (uc < 0 && u < nch && (r + ct >= tg)) { uc = u; x = v[u]; xi = inc; }
-            if (uc < 0) r += ct;
+        if (hb) {
+            uc = __builtin_ctzll(hb);
+            const unsigned long long cu = wave_bcast_u64(ci, uc), tu = wave_bcast_u64(ct, uc);
+            r = base + cu - tu;   // everything before chunk uc
+            x = s_tr[uc][lane];
+            xi = wave_scan_u64(x);
+        } else {
+            r = base + wave_bcast_u64(ci, CU - 1);   // past the register chunks
         }
         for (int u = CU; uc < 0 && u < nch; ++u) {   // past the register cache (n > ~134M points)
             const long long b = sb + 64LL * u + lane;
             const unsigned long long y = b < se ? bsum[b] : 0ull;
             const unsigned long long inc = wave_scan_u64(y);
-            const unsigned long long ct = wave_last_u64(inc);
-            if (r + ct >= tg) { uc = u; x = y; xi = inc; } else { r += ct; }
+            const unsigned long long ct2 = wave_last_u64(inc);
+            if (r + ct2 >= tg) { uc = u; x = y; xi = inc; } else { r += ct2; }
         }
         if (uc >= 0) {
             const long long b = sb + 64LL * uc + lane;
@@ -503,8 +547,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LM <= 8 ? P
                 const float cm = cmax[cl];
                 cb = cell_start[cl];
                 ce = cell_start[cl + 1];
+                // the cell's box once, then every candidate against it
+                int f[MAXD];
+                decode32<D>((unsigned)cl, g.G, f);
+                double blo[MAXD], bhi[MAXD];
+                cell_box<D>(g, f, f, blo, bhi);
                 for (int q = 0; q < L; ++q)
-                    if (kpp_reaches<D>(g, cl, s_cand[q], cm)) lmask |= 1u << q;
+                    if (kpp_reaches_box<D>(blo, bhi, s_cand[q], cm)) lmask |= 1u << q;
             }
             unsigned long long bits = __ballot(lmask != 0u);
             if (lane == 0) {
@@ -547,11 +596,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LM <= 8 ? P
                 int i0[MAXD], i1[MAXD];
 #pragma unroll
                 for (int a = 0; a < D; ++a) { i0[a] = s_i0[l][a]; i1[a] = s_i1[l][a]; }
-                cell = kpp_cube_cell<D>(g, i0, i1, it - s_off[l]);
+                int f[MAXD];
+                cell = kpp_cube_cell<D>(g, i0, i1, (unsigned)(it - s_off[l]), f);
                 const float cm = cmax[cell];
                 cb = cell_start[cell];
                 ce = cell_start[cell + 1];
-                reach = kpp_reaches<D>(g, cell, s_cand[l], cm);
+                reach = kpp_reaches_f<D>(g, f, s_cand[l], cm);
             }
             unsigned long long bits = __ballot(reach);
             if (k0 == 0) DBG_E(3);
@@ -662,11 +712,12 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
         bool reach = false;
         uint32_t cbl = 0u, cel = 0u;
         if (k0 + lane < ipw) {
-            celll = kpp_cube_cell<D>(g, i0, i1, itl);
+            int f[MAXD];
+            celll = kpp_cube_cell<D>(g, i0, i1, (unsigned)itl, f);
             const float cm = cmax[celll];
             cbl = cell_start[celll];
             cel = cell_start[celll + 1];
-            reach = kpp_reaches<D>(g, celll, best, cm);
+            reach = kpp_reaches_f<D>(g, f, best, cm);
         }
         unsigned long long bits = __ballot(reach);
         if (lane == 0) {
