@@ -231,6 +231,30 @@ __device__ __forceinline__ void kpp_cell_points(const float *__restrict__ xs, co
     }
 }
 
+// kpp_cell_points that also loads each point's caller row (perm) in the same
+// batch, so that apply's row-order updates (crow, block sums) do not wait for a
+// dependent perm load after the distances
+template <int D, int PPL, typename F>
+__device__ __forceinline__ void kpp_cell_points_rows(const float *__restrict__ xs, const float *__restrict__ closest,
+                                                     const uint32_t *__restrict__ perm, uint32_t b, uint32_t e,
+                                                     int lane, F &&f) {
+    for (uint32_t i0 = b + lane; i0 < e; i0 += 64u * PPL) {
+        float x[PPL][D], cl[PPL];
+        uint32_t rw[PPL];
+#pragma unroll
+        for (int u = 0; u < PPL; ++u) {
+            const uint32_t i = i0 + 64u * u;
+            const uint32_t ii = i < e ? i : i0;
+            kpp_point<D>(xs, ii, x[u]);
+            cl[u] = closest[ii];
+            rw[u] = perm[ii];
+        }
+#pragma unroll
+        for (int u = 0; u < PPL; ++u)
+            if (i0 + 64u * u < e) f(i0 + 64u * u, x[u], cl[u], rw[u]);
+    }
+}
+
 __device__ __forceinline__ float4 kpp_row_centre(const float *__restrict__ X, long long r, int D) {
     float v[4] = {0.f, 0.f, 0.f, 0.f};
     for (int a = 0; a < D; ++a) v[a] = X[r * D + a];
@@ -730,18 +754,24 @@ __global__ __launch_bounds__(256) void k_kpp_apply(const float *__restrict__ xs,
             const long long cell = (long long)__shfl((int)celll, src);   // cell ids < 2^31 (kpp grid <= 2^20 cells)
             const uint32_t b = (uint32_t)__shfl((int)cbl, src), e = (uint32_t)__shfl((int)cel, src);
             float mx = 0.f;
-            kpp_cell_points<D, KPP_PPL>(xs, closest, b, e, lane, [&](uint32_t i, const float (&x)[D], float cl) {
-                const float d = dist_canon<D>(x, best);
-                if (d < cl) {
-                    closest[i] = d;
-                    if (!dense) {
-                        const uint32_t r = perm[i];
+            if (dense) {   // (block-uniform) rows are rebuilt below
+                kpp_cell_points<D, KPP_PPL>(xs, closest, b, e, lane, [&](uint32_t i, const float (&x)[D], float cl) {
+                    const float d = dist_canon<D>(x, best);
+                    if (d < cl) closest[i] = d;
+                    mx = fmaxf(mx, fminf(d, cl));
+                });
+            } else {
+                kpp_cell_points_rows<D, KPP_PPL>(xs, closest, perm, b, e, lane,
+                                                 [&](uint32_t i, const float (&x)[D], float cl, uint32_t r) {
+                    const float d = dist_canon<D>(x, best);
+                    if (d < cl) {
+                        closest[i] = d;
                         crow[r] = d;
                         atomicAdd(&bsum[r >> KPP_OB_LOG], ~(kpp_w(cl, s) - kpp_w(d, s)) + 1ull);   // -= (mod 2^64)
                     }
-                }
-                mx = fmaxf(mx, fminf(d, cl));
-            });
+                    mx = fmaxf(mx, fminf(d, cl));
+                });
+            }
             mx = wave_max_f(mx);
             if (lane == 0) cmax[cell] = mx;
         }
