@@ -5,7 +5,7 @@
 #   drift      candidate-list reuse policy (PCM_DRIFT_KAPPA x PCM_DRIFT_ALPHA), 12.5M shard and config 3
 #   slab       8-slab proxy vs grid density (PCM_CELL_TARGET) x candidate blocks per coarse cell (PCM_CAND_BPC_RT)
 #   wpe LIB..  product build vs variant libraries tools/ab/lib_LIB.so (tools/build_variant.sh) at c3 / s12 / c5 shard
-#   kppgrid    k-means++ late-step eval grid (PCM_KPP_LATE_DIV)
+#   kppgrid    k-means++ late-step eval / apply grids (PCM_KPP_LATE_DIV, PCM_KPP_APPLY_DIV)
 #   unperm     sorted-order labels -> row order variants (PCM_UNPERM x PCM_UNPERM_WIN, tools/unperm_probe.py)
 #   split      multi-GPU call sequence on one GPU (an RCCL group of 1), eager and graph, at 12.5M and 100M
 # Output: gpurun_out/sw_PRESET/ and one summary line per run on stdout.
@@ -46,7 +46,9 @@ case $P in
          run s12_$so "${E[@]}" -- $S12; line "$so s12" $T/s12_$so.txt "$B"
          run c5_$so "${E[@]}" -- --n 62500000 --k 4096 --d 4; line "$so c5" $T/c5_$so.txt "$B"
        done ;;
-  kppgrid) for dv in 1 2 4 8; do PCM_KPP_LATE_DIV=$dv bash tools/kpp_prof.sh kg_$dv | sed "s/^/div=$dv /" | grep -v "call 0"; done ;;
+  kppgrid) for cfg in "1 4" "2 4" "4 4" "1 2" "1 8"; do set -- $cfg
+             PCM_KPP_LATE_DIV=$1 PCM_KPP_APPLY_DIV=$2 bash tools/kpp_prof.sh sw_kppgrid/e$1_a$2 | sed "s/^/eval 1\/$1 apply 1\/$2 /" | grep -v "call 0"
+           done ;;
   unperm) for cfg in "0 67108864" "1 200000000" "1 67108864" "1 33554432" "2 67108864" "2 33554432"; do set -- $cfg
             PCM_UNPERM=$1 PCM_UNPERM_WIN=$2 timeout -k 10 120 python tools/unperm_probe.py >> $T/log.txt 2>&1 || { tail -5 $T/log.txt; exit 1; }
             tail -1 $T/log.txt
