@@ -199,6 +199,13 @@ void rs_plan(long long n, unsigned bits, RsPlan &p) {
     p.total = o;
 }
 
+// XCD-aware block orders (xcd_block), a bit mask: 1 the sort scatters, 2 k_lloyd1's tiles, 4 the label
+// gathers
+static int xcd_mode() {
+    static const int m = [] { const char *v = std::getenv("PCM_XCD"); return v ? std::atoi(v) : 7; }();
+    return m;
+}
+
 // Sort the caller's rows X into cell order: AoSoA-4 xs (zero padded to npad)
 // and perm (sorted position -> row).
 template <typename TT, int D>
@@ -225,7 +232,7 @@ int rs_sort(const TT *X, long long n, long long npad, const Grid &g, int with_su
         LAUNCHCHK();
 #define PCM_RS_SCATTER(FX, TX)                                                                                      \
     k_rs_scatter<TT, D, FX, TX><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, goff, segb, rout, \
-                                                        xs, perm, dmaps ? dmaps + (size_t)q * n : nullptr)
+                                                        xs, perm, dmaps ? dmaps + (size_t)q * n : nullptr, xcd_mode() & 1)
         if (from_x && to_xs) PCM_RS_SCATTER(true, true);
         else if (from_x) PCM_RS_SCATTER(true, false);
         else if (to_xs) PCM_RS_SCATTER(false, true);
@@ -927,6 +934,7 @@ static int assign_ls(const pcm_engine *e) {
 
 static LloydArgs lloyd_args(pcm_engine *e) {
     LloydArgs A{};
+    A.xcd = (xcd_mode() >> 1) & 1;
     A.xs = e->xs;
     A.xz = e->use_xz ? e->xz : nullptr;
     A.tmeta = e->use_xz ? e->tmeta : nullptr;
@@ -1349,15 +1357,16 @@ int pcm_labels(pcm_engine *e, int32_t *out, void *stream) {
             LT *mid = (LT *)e->ws;   // 256-B aligned scratch
             const uint32_t *m1 = e->dmap + e->n;   // the second pass's map: 16-B aligned iff n % 4 == 0
             const int g4 = (int)blocks_for((e->n + 3) / 4);
+            const int xg = (xcd_mode() >> 2) & 1;
             if (((uintptr_t)m1 & 15u) == 0)
-                k_lab_gather4<LT, LT, true, true><<<g4, 256, 0, s>>>(m1, (const LT *)e->lab, e->n, mid);
+                k_lab_gather4<LT, LT, true, true><<<g4, 256, 0, s>>>(m1, (const LT *)e->lab, e->n, mid, xg);
             else
-                k_lab_gather4<LT, LT, false, true><<<g4, 256, 0, s>>>(m1, (const LT *)e->lab, e->n, mid);
+                k_lab_gather4<LT, LT, false, true><<<g4, 256, 0, s>>>(m1, (const LT *)e->lab, e->n, mid, xg);
             LAUNCHCHK();
             if (a16)
-                k_lab_gather4<LT, int32_t, true, true><<<g4, 256, 0, s>>>(e->dmap, mid, e->n, out);
+                k_lab_gather4<LT, int32_t, true, true><<<g4, 256, 0, s>>>(e->dmap, mid, e->n, out, xg);
             else
-                k_lab_gather4<LT, int32_t, true, false><<<g4, 256, 0, s>>>(e->dmap, mid, e->n, out);
+                k_lab_gather4<LT, int32_t, true, false><<<g4, 256, 0, s>>>(e->dmap, mid, e->n, out, xg);
             LAUNCHCHK();
             return 0;
         }

@@ -1357,6 +1357,18 @@ template <int D, int LS = LSLOT> struct AccL {
     static constexpr size_t bytes_crowded = ((size_t)words * 4 + 7) / 8 * 8 + (size_t)gwords * 8;
 };
 
+// XCD-aware block order (a speed choice only: every kernel using it is
+// correct under any dispatch).  The dispatcher deals a grid's blocks round-robin
+// over the 8 XCDs, each with its own L2, so by default neighbouring chunks or
+// tiles -- which share the cache lines at their boundaries and often their
+// cell's records -- run on different XCDs.  This maps the blocks one XCD
+// receives (b % 8 labels them) onto one contiguous range of chunk ids, in
+// dispatch order; bijective on [0, nb) for any nb.
+__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned nb) {
+    const unsigned q = nb >> 3, r = nb & 7u, x = b & 7u, k = b >> 3;
+    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + k;
+}
+
 struct LloydArgs {
     const void *xs;                 // packed AoS [npad][D] of T, cell order
     const unsigned *xz;             // compressed 8-B records (fp32 D = 3 tiles with tmeta .w bit 31), or null
@@ -1380,6 +1392,7 @@ struct LloydArgs {
     const float4 *tl_rec;           // [tile][TLCAP] records of the tile lists (k_tile_cand)
     const float4 *tbox;             // crowded layouts: [tile][2] exact point box (lo, hi), else null
     const int32_t *tl_lab;
+    int xcd;                        // k_lloyd1 takes its tile through xcd_block
 };
 
 struct TileL {
@@ -1664,7 +1677,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(lloyd1_wpe_
     __shared__ float skey[LCAP];
     __shared__ int32_t sid[LS];
     const int tid = threadIdx.x;
-    const unsigned t = blockIdx.x;
+    const unsigned t = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     // the gate flags, the device tile count and the tile record are loaded
     // together (one memory latency, not three in a row): the tiles buffer holds
     // ntiles_cap >= gridDim.x records, so the record load is in bounds before

@@ -162,7 +162,8 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_scatter(const T *__restrict__ X, 
                                                        const uint32_t *__restrict__ goff,
                                                        const uint32_t *__restrict__ segb,
                                                        PRec<T, D> *__restrict__ rout, T *__restrict__ xs,
-                                                       uint32_t *__restrict__ perm, uint32_t *__restrict__ dmap) {
+                                                       uint32_t *__restrict__ perm, uint32_t *__restrict__ dmap,
+                                                       int xcd) {
     constexpr int IPT = RsCfg<T, D>::IPT, CH = RsCfg<T, D>::CH, PW = CH / RS_NWV;
     __shared__ PRec<T, D> stage[CH];
     __shared__ uint8_t sdig[CH];
@@ -172,7 +173,11 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_scatter(const T *__restrict__ X, 
     __shared__ uint32_t wtot[4];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int k = tid; k < RS_NWV * RS_DIG; k += RS_TPB) (&wc[0][0])[k] = 0u;
-    const long long base = (long long)blockIdx.x * CH;
+    // chunk through xcd_block: a chunk's digit runs end in lines shared with the
+    // next chunk's runs of the same digits, and those partial lines merge in one
+    // L2 when both chunks run on the same XCD
+    const unsigned chunk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const long long base = (long long)chunk * CH;
     const uint32_t mask = (1u << width) - 1u;
     const unsigned long long lt = (1ull << lane) - 1ull;
     // wave wv owns the PW consecutive items [base + wv * PW, ...), 64 per round
@@ -225,8 +230,8 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_scatter(const T *__restrict__ X, 
             for (int w = 0; w < wv; ++w) pre += wtot[w];
             const uint32_t ex = pre + v - tot;
             dstart[tid] = ex;
-            gdelta[tid] = (long long)goff[(long long)blockIdx.x * RS_DIG + tid] +
-                          (long long)segb[(long long)(blockIdx.x / RS_SEG) * RS_DIG + tid] - (long long)ex;
+            gdelta[tid] = (long long)goff[(long long)chunk * RS_DIG + tid] +
+                          (long long)segb[(long long)(chunk / RS_SEG) * RS_DIG + tid] - (long long)ex;
         }
     }
     __syncthreads();
@@ -285,8 +290,11 @@ __global__ __launch_bounds__(256) void k_cell_starts_xs(const T *__restrict__ xs
 // (one output per thread moved ~1.9 TB/s: two dependent 2-B accesses a lane).
 template <typename LT, typename OT, bool VM, bool VO>
 __global__ __launch_bounds__(256) void k_lab_gather4(const uint32_t *__restrict__ dmap, const LT *__restrict__ src,
-                                                     long long n, OT *__restrict__ dst) {
-    const long long i4 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * 4;
+                                                     long long n, OT *__restrict__ dst, int xcd) {
+    // xcd_block: the source runs of neighbouring sort chunks are adjacent and
+    // share lines, which then come into one L2
+    const unsigned b = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const long long i4 = (b * (long long)blockDim.x + threadIdx.x) * 4;
     if (i4 >= n) return;
     if (i4 + 4 > n) {
         for (long long i = i4; i < n; ++i) dst[i] = (OT)src[dmap[i]];
