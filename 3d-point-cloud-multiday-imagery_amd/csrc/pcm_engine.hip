@@ -8,6 +8,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <vector>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -66,6 +67,7 @@ struct pcm_engine {
     uint4 *tmeta = nullptr;          // per-tile compression records
     unsigned long long *zpts = nullptr;   // points in compressed tiles (device counter)
     bool use_xz = false;             // the current layout has a compressed stream
+    bool tiles_lpt = false;          // tiles ordered longest candidate list first (PCM_TILE_LPT, A/B)
     size_t cap_xz = 0, cap_tmeta = 0;
     // crowded layouts (tight clusters): Morton levels of the in-cell order and the tile lists
     int zlev = 0;
@@ -752,6 +754,7 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
     LAUNCHCHK();
     k_tile_write<<<blocks_for(nc), 256, 0, s>>>(e->cell_start, e->tile_off, nc, e->tiles, e->tile_cap);
     LAUNCHCHK();
+    e->tiles_lpt = false;
     // the exact tile count for the grids of the per-tile kernels (the bound
     // ntiles_cap launched ~1.7x as many blocks at config 3, the excess exiting
     // after one memory latency: a drain tail on every assign launch)
@@ -792,6 +795,44 @@ int pcm_layout_build(pcm_engine *e, const void *X, const int32_t *q, int64_t gid
 
 static int launch_candidates(pcm_engine *e, hipStream_t s, int gate);
 
+// Longest-list-first tile order: the tile records (and their compression
+// records) sorted by descending candidate-list length of their cell at the
+// first lists, so k_lloyd1 dispatches its longest-lived blocks first and the
+// short ones fill the tail (a block's lifetime follows its list length,
+// DESIGN.md §4).  Where the tiles are few generations of resident blocks (the
+// 8-way slab: 4096 tiles, 37.1 vs 39.1 us per assign) or D = 4 (config-5 shard,
+// 299 vs 307 us) it pays; config 3's 32768 D = 3 tiles keep their spatial order
+// and the XCD ranges (profiles/rd6_tile_lpt_ab.txt).  The statistics are exact
+// integers, so the order changes no result.  PCM_TILE_LPT = 0 / 1 forces it.
+static int tiles_order_lpt(pcm_engine *e, hipStream_t s) {
+    static const int mode = [] { const char *v = std::getenv("PCM_TILE_LPT"); return v ? std::atoi(v) : -1; }();
+    const bool want = mode == 1 || (mode < 0 && (e->d >= 4 || e->ntiles <= 16LL * e->num_cu));
+    if (!want || e->zlev > 0 || e->ntiles < 2) return 0;   // crowded layouts: tile boxes and lists are per tile
+    const unsigned nt = (unsigned)e->ntiles;
+    size_t sort_bytes = 0;
+    if (rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (uint32_t *)nullptr, (size_t)nt, 0u, 16u, s) != hipSuccess)
+        return fail(PCM_E_HIP, "tile order: sort size");
+    const size_t o_k1 = align_up((size_t)nt * 4), o_v0 = o_k1 + align_up((size_t)nt * 4), o_v1 = o_v0 + align_up((size_t)nt * 4),
+                 o_t2 = o_v1 + align_up((size_t)nt * 4), o_m2 = o_t2 + align_up((size_t)nt * 16),
+                 o_tmp = o_m2 + align_up((size_t)nt * 16), need = o_tmp + sort_bytes;
+    if (ensure(e->ws, e->cap_ws, need) != hipSuccess) return fail(PCM_E_NOMEM, "tile order scratch");
+    char *wb = (char *)e->ws;
+    uint32_t *k0 = (uint32_t *)wb, *k1 = (uint32_t *)(wb + o_k1), *v0 = (uint32_t *)(wb + o_v0), *v1 = (uint32_t *)(wb + o_v1);
+    uint4 *t2 = (uint4 *)(wb + o_t2), *m2 = (uint4 *)(wb + o_m2);
+    k_tile_lpt_keys<<<blocks_for(nt), 256, 0, s>>>(e->tiles, e->fc_cnt, nt, k0, v0);
+    LAUNCHCHK();
+    size_t sb = sort_bytes;
+    if (rocprim::radix_sort_pairs((void *)(wb + o_tmp), sb, k0, k1, v0, v1, (size_t)nt, 0u, 16u, s) != hipSuccess)
+        return fail(PCM_E_HIP, "tile order: sort");
+    k_tile_gather<<<blocks_for(nt), 256, 0, s>>>(e->tiles, e->use_xz ? e->tmeta : nullptr, v1, nt, t2, m2);
+    LAUNCHCHK();
+    HIPCHK(hipMemcpyAsync(e->tiles, t2, (size_t)nt * sizeof(uint4), hipMemcpyDeviceToDevice, s));
+    if (e->use_xz) HIPCHK(hipMemcpyAsync(e->tmeta, m2, (size_t)nt * sizeof(uint4), hipMemcpyDeviceToDevice, s));
+    e->tiles_lpt = true;
+    return 0;
+}
+
 int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void *stream) {
     if (!e || !C0) return fail(PCM_E_ARG, "bad argument");
     if (!e->layout_ready) return fail(PCM_E_STATE, "layout not built");
@@ -820,7 +861,8 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
     HIPCHK(hipMemcpyAsync(e->ctrl, &e->ctrl_host, sizeof(Ctrl), hipMemcpyHostToDevice, s));
     e->fit_ready = true;
     // candidate lists of C0 (later iterations get theirs from k_lists / the resume path)
-    return launch_candidates(e, s, 0);
+    if (int rc2 = launch_candidates(e, s, 0)) return rc2;
+    return tiles_order_lpt(e, s);
 }
 
 // Candidate blocks per coarse cell: enough blocks to fill the chip on small
@@ -934,7 +976,7 @@ static int assign_ls(const pcm_engine *e) {
 
 static LloydArgs lloyd_args(pcm_engine *e) {
     LloydArgs A{};
-    A.xcd = (xcd_mode() >> 1) & 1;
+    A.xcd = ((xcd_mode() >> 1) & 1) && !e->tiles_lpt;   // an ordered tile list is dealt round-robin
     A.xs = e->xs;
     A.xz = e->use_xz ? e->xz : nullptr;
     A.tmeta = e->use_xz ? e->tmeta : nullptr;

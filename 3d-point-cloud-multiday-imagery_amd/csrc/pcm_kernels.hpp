@@ -385,6 +385,28 @@ __global__ __launch_bounds__(256) void k_tile_write(const uint32_t *__restrict__
     }
 }
 
+// Longest-list-first tile order (pcm_fit_begin): key = 0xffff - the list
+// length of the tile's cell at the first lists (FULL: the longest), value = the
+// tile; a stable radix sort, then the records gathered in that order.
+__global__ __launch_bounds__(256) void k_tile_lpt_keys(const uint4 *__restrict__ tiles, const uint32_t *__restrict__ fc_cnt,
+                                                       unsigned nt, uint32_t *__restrict__ key, uint32_t *__restrict__ idx) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= nt) return;
+    const uint32_t c = fc_cnt[tiles[t].x];
+    key[t] = 0xffffu - (c == FULL ? 0xffffu : min(c, 0xfffeu));
+    idx[t] = t;
+}
+
+__global__ __launch_bounds__(256) void k_tile_gather(const uint4 *__restrict__ tiles, const uint4 *__restrict__ tmeta,
+                                                     const uint32_t *__restrict__ idx, unsigned nt,
+                                                     uint4 *__restrict__ t2, uint4 *__restrict__ m2) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= nt) return;
+    const uint32_t j = idx[t];
+    t2[t] = tiles[j];
+    if (tmeta) m2[t] = tmeta[j];
+}
+
 // Compressed point stream (fp32, D = 3).  Inside one tile (one cell, <= TILE
 // points) each axis spans a short range, so every coordinate's fp32 bit pattern
 // is the tile's minimum pattern on that axis plus a small unsigned delta (the
