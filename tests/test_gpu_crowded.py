@@ -1,4 +1,4 @@
-"""GPU: crowded layouts (tile lists, DESIGN.md §4 "Crowded cells") are exact.
+"""GPU: crowded layouts (tile lists: csrc/pcm_kernels.hpp "crowded cells: tile lists", k_tile_cand) are exact.
 
 Tight clusters put a whole cluster and its hundreds of centres into one grid
 cell: the cell's list overflows CAPF (FULL) and, without tile lists, every
