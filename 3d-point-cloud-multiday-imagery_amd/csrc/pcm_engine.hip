@@ -1132,12 +1132,28 @@ static int iter_global_impl(pcm_engine *e, hipStream_t s, bool from_partials, bo
             const bool fused_on = !(fz && std::atoi(fz) == 0);
             if (fused_on && D <= 3 && !split_coarse(e) && e->k <= 2 * CAND_TPB) {
                 const int bpc = cand_bpc(e);
+                const int nlist = (int)(e->g.ncoarse * bpc);
                 auto fused = [&](auto RR) {
-                    k_updlists<D, decltype(RR)::value><<<(int)(e->g.ncoarse * bpc), CAND_TPB,
-                                                         (size_t)e->k * sizeof(float4), s>>>(
-                        from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->cref,
-                        e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin, e->g,
-                        e->fc_cnt, e->fc_rec, e->fc_lab, bpc);
+                    constexpr int RV = decltype(RR)::value;
+                    const size_t lds = (size_t)e->k * sizeof(float4);
+                    // a dedicated publisher block when one more block still fits the residency
+                    // (PCM_UPD_PUB=0: always the last arriver -- A/B only)
+                    static const int pub_env = [] { const char *v = std::getenv("PCM_UPD_PUB"); return v ? std::atoi(v) : 1; }();
+                    int per_cu = 0;
+                    const bool pub = pub_env &&
+                        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_updlists<D, RV, true>,
+                                                                     CAND_TPB, lds) == hipSuccess &&
+                        (long long)nlist + 1 <= (long long)per_cu * e->num_cu;
+                    if (pub)
+                        k_updlists<D, RV, true><<<nlist + 1, CAND_TPB, lds, s>>>(
+                            from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->cref,
+                            e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin, e->g,
+                            e->fc_cnt, e->fc_rec, e->fc_lab, bpc);
+                    else
+                        k_updlists<D, RV, false><<<nlist, CAND_TPB, lds, s>>>(
+                            from_partials ? nullptr : e->stats, e->partials, e->k, e->qe, e->held, e->prev, e->C, e->cref,
+                            e->hist_changed, e->hist_shift, e->ctrl, e->drift_alpha, e->drift_kappa * wmin, e->g,
+                            e->fc_cnt, e->fc_rec, e->fc_lab, bpc);
                 };
                 if (e->k <= CAND_TPB) fused(std::integral_constant<int, 1>{});
                 else fused(std::integral_constant<int, 2>{});

@@ -1186,11 +1186,13 @@ __global__ __launch_bounds__(CAND_TPB) void k_coarse(Grid g, const float4 *__res
 // threads per cell, every load of a cell's count and ids issued in parallel.
 template <int D, int TPB = CAND_TPB>
 __device__ __forceinline__ void refresh_body(const Grid &g, const float4 *cn, const uint32_t *__restrict__ fc_cnt,
-                                             float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab) {
+                                             float4 *__restrict__ fc_rec, const int32_t *__restrict__ fc_lab,
+                                             unsigned nblk = 0u) {   // list blocks (0: gridDim.x)
     constexpr int PER = 16, CPB = TPB / PER;   // threads per cell, cells per block pass
     const int sub = (int)threadIdx.x % PER;
+    const unsigned nb = nblk ? nblk : gridDim.x;
     for (long long cell = (long long)blockIdx.x * CPB + (int)threadIdx.x / PER; cell < g.ncells;
-         cell += (long long)gridDim.x * CPB) {
+         cell += (long long)nb * CPB) {
         const uint32_t m = fc_cnt[cell];
         if (m == FULL) continue;
         for (uint32_t p = sub; p < m; p += PER) fc_rec[cell * CAPF + p] = cn[fc_lab[cell * CAPF + p]];
@@ -2763,7 +2765,12 @@ __global__ __launch_bounds__(TPB) void k_lists(Grid g, const float4 *__restrict_
 // buffer, the shift tree of oracle/lloyd_ref.py shift_total, history and flags
 // -- and every block rebuilds or refreshes its own cells' lists from the LDS
 // centres.  Replaces k_upd1 + k_lists (two launches, ~16 us at an 8-way slab).
-template <int D, int R>
+// PUB (round 6; the host takes it when one more block fits the residency, e.g.
+// the 8-way slab's 256 list blocks): the LAST block of the grid builds no lists
+// and is the publisher -- it waits (bounded, s_sleep) until the list blocks have
+// arrived, right after their centres, and publishes while they still build
+// their lists, instead of after its own lists; a wait past 2 s sets done = 5.
+template <int D, int R, bool PUB = false>
 __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     unsigned long long *__restrict__ stats_in, unsigned long long *__restrict__ partials, int K, QExp qe,
     unsigned long long *__restrict__ held, unsigned long long *__restrict__ prev, float4 *__restrict__ C,
@@ -2856,7 +2863,14 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
     // lists read only the LDS centres.  The publisher is the last block to
     // ARRIVE (here), not the last to finish its lists, so its extra work lands
     // on a block of ordinary length.
-    const unsigned tk = arrive_issue(&ctrl->u_arrive, (unsigned long long)__builtin_amdgcn_readfirstlane(wv == 0 ? 1 : 0));
+    const bool pub_blk = PUB && blockIdx.x == gridDim.x - 1u;   // the dedicated publisher (PUB)
+    const unsigned nlist = PUB ? gridDim.x - 1u : gridDim.x;
+    unsigned tk = 0u;
+    if constexpr (PUB) {
+        if (!pub_blk && tid == 0) __hip_atomic_fetch_add(&ctrl->u_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        tk = arrive_issue(&ctrl->u_arrive, (unsigned long long)__builtin_amdgcn_readfirstlane(wv == 0 ? 1 : 0));
+    }
     // the decisions of upd_publish, identical in every block (same data, order-free maxima)
     auto decide = [&](unsigned long long &n_empty, double &dmax, double &smax, bool &rebuild, double &dl_new) {
         n_empty = 0ull; dmax = 0.0; smax = 0.0;
@@ -2889,20 +2903,38 @@ __global__ __launch_bounds__(CAND_TPB) void k_updlists(
         }
         DBG_T(15);
         // a halted iteration (identical decision in every block) builds no lists
-        if (n_empty == 0ull) {
+        if (n_empty == 0ull && !pub_blk) {
             DBG_T(14);
             // this block's cells: rebuilt at the new centres with the new budget, or refreshed
             if (rebuild) cand_body<D, 4>(g, cstage, K, fc_cnt, fc_rec, fc_lab, bpc, dl_new, CoarseL{});
-            else refresh_body<D>(g, cstage, fc_cnt, fc_rec, fc_lab);
+            else refresh_body<D>(g, cstage, fc_cnt, fc_rec, fc_lab, nlist);
         }
     }
-    if (wv == 0) {
-        const unsigned place = arrive_read(tk);
-        if (lane == 0) s_last = place == gridDim.x - 1u;
+    if constexpr (PUB) {
+        if (!pub_blk) return;
+        if (wv == 0) {   // every list block arrives right after its centres: a bounded wait
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+            unsigned ok = 1u;
+            while (__hip_atomic_load(&ctrl->u_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nlist) {
+                __builtin_amdgcn_s_sleep(2);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) { ok = 0u; break; }
+            }
+            if (lane == 0) s_last = ok;
+        }
+        __syncthreads();   // s_last
+        if (!s_last) {
+            if (tid == 0) ctrl->done = 5u;   // the fit is void (lloyd.run raises)
+            return;
+        }
+    } else {
+        if (wv == 0) {
+            const unsigned place = arrive_read(tk);
+            if (lane == 0) s_last = place == gridDim.x - 1u;
+        }
+        __syncthreads();   // s_last
+        if (!s_last) return;
     }
-    __syncthreads();   // s_last
     DBG_T(3);
-    if (!s_last) return;
     // ---- the publisher: every other block's loads have returned.  It reads the
     // rows again (L2; nobody has written them): prev := rows, the next
     // accumulation target := 0 and (unless halted: the relocation needs the old

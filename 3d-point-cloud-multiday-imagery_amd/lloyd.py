@@ -71,6 +71,7 @@ def _world(group):
 
 
 XCHG_FAILED = 4     # pcm_status.done: a peer exchange timed out
+UPD_FAILED = 5      # pcm_status.done: k_updlists' publisher timed out waiting for its list blocks
 SLAB_BINS = 16384   # slab histogram resolution (pcm_shard_hist's LDS bound)
 SLAB_MAXP = 16      # PCM_SHARD_MAXP: ranks a slab partition can address (uint8 owner table, LDS counters)
 
@@ -290,6 +291,10 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, gra
         if st["done"] == XCHG_FAILED:
             from ._lib import PcmError
             raise PcmError("pcm_amd.lloyd: the peer statistics exchange timed out (a rank stopped pushing); "
+                           "the fit is void")
+        if st["done"] == UPD_FAILED:
+            from ._lib import PcmError
+            raise PcmError("pcm_amd.lloyd: the update's publisher timed out waiting for its list blocks; "
                            "the fit is void")
         if st["halt"]:
             recs = engine.reloc_candidates(int(st["n_empty"]))

@@ -57,7 +57,8 @@ enum pcm_err {
 typedef struct pcm_status {
     uint32_t halt;       /* 1: empty clusters need relocation (pcm_reloc_*) */
     uint32_t done;       /* 0 running, 1 strict label convergence, 2 shift<=tol, 3 max_iter,
-                            4 a peer exchange timed out (pcm_iter_exchange; the fit is void) */
+                            4 a peer exchange timed out (pcm_iter_exchange; the fit is void),
+                            5 the update's publisher block timed out waiting for its list blocks (void) */
     uint32_t iter;       /* completed Lloyd iterations */
     uint32_t n_empty;    /* empty clusters seen by the halted iteration */
     double inertia;      /* local inertia of the last pcm_final (= pcm_inertia_value of the fields below) */

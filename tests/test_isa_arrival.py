@@ -65,6 +65,8 @@ def _functions(text, name):
 def test_updlists_arrival_register_untouched_until_its_wait(disasm):
     seen = 0
     for sym, lines in _functions(disasm, "k_updlists"):
+        if "Lb1EE" in sym:   # PUB = true: a dedicated publisher waits for plain arrivals (no returned place)
+            continue
         lines = [ln for ln in lines if ln]
         at = [i for i, ln in enumerate(lines) if re.match(r"global_atomic_add v\d+, v\[\d+:\d+\], v\d+, off sc0$", ln)]
         assert len(at) == 1, (sym, [lines[i] for i in at])
@@ -82,4 +84,4 @@ def test_updlists_arrival_register_untouched_until_its_wait(disasm):
                 waited = True
         assert waited, f"{sym}: no s_waitcnt vmcnt(0) between the arrival and its read"
         seen += 1
-    assert seen >= 2   # the D = 1..3 (and 4) x R = 1, 2 instantiations
+    assert seen >= 2   # the D = 1..3 x R = 1, 2 last-arriver instantiations
