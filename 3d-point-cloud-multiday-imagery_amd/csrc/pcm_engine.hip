@@ -208,6 +208,14 @@ static int xcd_mode() {
     return m;
 }
 
+// 16-B row loads of the caller's X in the sort's first count pass (X 16-B aligned; PCM_SORT_VEC=0: the
+// 4-B loads, A/B).  The same staged through LDS in the first scatter measured 899-901 -> 909-916 us
+// (profiles/rd6_sort_count_vec.txt), so the scatter keeps its 4-B loads.
+static int sort_vec(const void *X) {
+    static const int m = [] { const char *v = std::getenv("PCM_SORT_VEC"); return v ? std::atoi(v) : 1; }();
+    return ((uintptr_t)X & 15u) == 0u ? m : 0;
+}
+
 // Sort the caller's rows X into cell order: AoSoA-4 xs (zero padded to npad)
 // and perm (sorted position -> row).
 template <typename TT, int D>
@@ -225,7 +233,7 @@ int rs_sort(const TT *X, long long n, long long npad, const Grid &g, int with_su
         R *rout = to_xs ? nullptr : ((q & 1) ? rb : ra);
         if (from_x)
             k_rs_count<TT, D, true><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, hist,
-                                                             ((uintptr_t)X & 15u) == 0u ? 1 : 0);
+                                                             sort_vec(X) & 1);
         else
             k_rs_count<TT, D, false><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, hist, 0);
         LAUNCHCHK();
