@@ -451,26 +451,45 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     // the whole tile (<= TILE = 16 x 256 points) in registers: every load in
     // flight at once, one read of xs (a strided loop waited one latency per
-    // round, twice: 505-530 us for 100M points)
-    constexpr int PPT = TILE / 256;
-    unsigned bits[PPT][3];
+    // round, twice: 505-530 us for 100M points).  Round 6: a thread takes whole
+    // AoSoA-4 groups -- 4 consecutive points, three 16-B loads (x4, y4, z4) --
+    // instead of one coordinate word per point and axis (4-B loads at a 12-B
+    // lane stride), and writes a full group's records as two 16-B stores
+    constexpr int GPT = TILE / 1024 + 1;   // groups per thread (a tile spans <= TILE / 4 + 1 groups)
+    const unsigned g0 = start >> 2, g1 = (end + 3u) >> 2;
+    const float4 *xs4 = reinterpret_cast<const float4 *>(xs);
+    float4 q[GPT][3];
 #pragma unroll
-    for (int u = 0; u < PPT; ++u) {
-        const unsigned i = start + tid + 256u * u;
+    for (int u = 0; u < GPT; ++u) {
+        const unsigned gg = g0 + (unsigned)tid + 256u * u;
+        if (gg < g1) {
 #pragma unroll
-        for (int a = 0; a < 3; ++a) bits[u][a] = i < end ? __float_as_uint(xs[xs_index<3>(i, a)]) : 0u;
+            for (int a = 0; a < 3; ++a) q[u][a] = xs4[(size_t)gg * 3 + a];
+        } else {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) q[u][a] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
+    auto word = [&](int u, int a, int k) -> unsigned {
+        const float4 &v = q[u][a];
+        return __float_as_uint(k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)));
+    };
     unsigned mn[3] = {~0u, ~0u, ~0u}, mx[3] = {0u, 0u, 0u}, sor[3] = {0u, 0u, 0u}, sand[3] = {1u, 1u, 1u};
 #pragma unroll
-    for (int u = 0; u < PPT; ++u) {
-        if (start + tid + 256u * u >= end) continue;
+    for (int u = 0; u < GPT; ++u) {
+        const unsigned gg = g0 + (unsigned)tid + 256u * u;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const unsigned b = bits[u][a];
-            mn[a] = min(mn[a], b);
-            mx[a] = max(mx[a], b);
-            sor[a] |= b >> 31;
-            sand[a] &= b >> 31;
+        for (int k = 0; k < 4; ++k) {
+            const unsigned i = 4u * gg + (unsigned)k;
+            if (gg >= g1 || i < start || i >= end) continue;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const unsigned b = word(u, a, k);
+                mn[a] = min(mn[a], b);
+                mx[a] = max(mx[a], b);
+                sor[a] |= b >> 31;
+                sand[a] &= b >> 31;
+            }
         }
     }
     __shared__ unsigned smn[4][3], smx[4][3], sso[4][3], ssa[4][3];
@@ -509,18 +528,35 @@ __global__ __launch_bounds__(256) void k_tile_compress(const float *__restrict__
     __syncthreads();
     const uint4 m = meta;
     if (!(m.w >> 31)) return;
-    const unsigned w0 = m.w & 0xffu, w1 = (m.w >> 8) & 0xffu, w2 = (m.w >> 16) & 0xffu;
+    const unsigned w0 = m.w & 0xffu, w2 = (m.w >> 16) & 0xffu;
 #pragma unroll
-    for (int u = 0; u < PPT; ++u) {
-        const unsigned i = start + tid + 256u * u;
-        if (i >= end) continue;
-        const unsigned long long d0 = bits[u][0] - m.x;
-        const unsigned long long d1 = bits[u][1] - m.y;
-        const unsigned long long d2 = bits[u][2] - m.z;
-        const unsigned long long v = d0 | (d1 << w0) | (d2 << (64u - w2));
-        const size_t g = zword(i);
-        xz[g] = (unsigned)v;
-        xz[g + ZHI] = (unsigned)(v >> 32);
+    for (int u = 0; u < GPT; ++u) {
+        const unsigned gg = g0 + (unsigned)tid + 256u * u;
+        if (gg >= g1) continue;
+        unsigned lw[4], hw[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned long long d0 = word(u, 0, k) - m.x;
+            const unsigned long long d1 = word(u, 1, k) - m.y;
+            const unsigned long long d2 = word(u, 2, k) - m.z;
+            const unsigned long long v = d0 | (d1 << w0) | (d2 << (64u - w2));
+            lw[k] = (unsigned)v;
+            hw[k] = (unsigned)(v >> 32);
+        }
+        const unsigned i0 = 4u * gg;
+        const size_t zg = zword(i0);   // 4 consecutive words, 16-B aligned (i0 % 4 == 0, same 256-point block)
+        if (i0 >= start && i0 + 4u <= end) {
+            *reinterpret_cast<uint4 *>(xz + zg) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+            *reinterpret_cast<uint4 *>(xz + zg + ZHI) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        } else {   // a group at the tile's edge: only this tile's points
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const unsigned i = i0 + (unsigned)k;
+                if (i < start || i >= end) continue;
+                xz[zg + k] = lw[k];
+                xz[zg + k + ZHI] = hw[k];
+            }
+        }
     }
 }
 
