@@ -8,6 +8,9 @@
 #   kppgrid    k-means++ late-step eval / apply grids (PCM_KPP_LATE_DIV, PCM_KPP_APPLY_DIV)
 #   unperm     sorted-order labels -> row order variants (PCM_UNPERM x PCM_UNPERM_WIN, tools/unperm_probe.py)
 #   split      multi-GPU call sequence on one GPU (an RCCL group of 1), eager and graph, at 12.5M and 100M
+#   lpt        longest-list-first tile order (PCM_TILE_LPT): parity subset, config-5 shard + 8-slab, 12.5M split, config 3
+#   pub        k_updlists' dedicated publisher block (PCM_UPD_PUB): parity subset, 8-slab A/B, a kernel trace
+#   slabcap    8-slab proxy vs tile cap (PCM_TILE_CAP) and the tile order
 # Output: gpurun_out/sw_PRESET/ and one summary line per run on stdout.
 set -o pipefail
 P=$1; shift
@@ -56,5 +59,26 @@ case $P in
   split) for n in 12500000 100000000; do for g in --no-graph ""; do
            run b_$n$g -- --split $g --n $n; line "n=$n $g" $T/b_$n$g.txt "round(d['ms_per_step']*1e3,1), 'us/iter', d['breakdown_ms_per_iter']"
          done; done ;;
+  lpt) export PYTHONUNBUFFERED=1
+       timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_compressed.py tests/test_gpu_xchg.py tests/test_gpu_multirank.py -m gpu -x -q --timeout 300 --timeout-method thread > $T/pytest.txt 2>&1 || { tail -30 $T/pytest.txt; exit 1; }
+       tail -1 $T/pytest.txt
+       bash tools/ab_c5.sh sw_lpt/c5 PCM_TILE_LPT "0 -1" 2 || exit 1
+       for v in 0 -1 0 -1; do
+         PCM_TILE_LPT=$v timeout -k 10 200 python bench.py --split --no-cpu --fit-iters 0 --n 12500000 > $T/split_$v.json 2>&1 || { tail -5 $T/split_$v.json; exit 1; }
+         line "split12.5M LPT=$v" $T/split_$v.json "round(d['ms_per_step']*1e3,1), d['breakdown_ms_per_iter']['assign']"
+       done
+       bash tools/ab_env.sh sw_lpt/c3 PCM_TILE_LPT "0 -1" 2 ;;
+  pub) export PYTHONUNBUFFERED=1
+       timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_xchg.py tests/test_gpu_multirank.py tests/test_gpu_crowded.py -m gpu -x -q --timeout 300 --timeout-method thread > $T/pytest.txt 2>&1 || { tail -30 $T/pytest.txt; exit 1; }
+       tail -1 $T/pytest.txt
+       for r in 1 2; do for v in 0 1; do
+         PCM_UPD_PUB=$v timeout -k 10 200 python bench.py --slab-of 8 --steps 20 --warmup 3 > $T/s8_${v}_$r.json 2>&1 || { tail -5 $T/s8_${v}_$r.json; exit 1; }
+         line "slab8 PUB=$v" $T/s8_${v}_$r.json "'us/rank', round(d['value'],1), 'step', d['per_rank_us']['step'], 'bitwise', d['centres_bitwise_equal_single_engine']"
+       done; done
+       bash tools/prof_proxy.sh sw_pub/prof --exchange peer ;;
+  slabcap) for r in 1 2; do for cfg in "4096 -1" "3072 1" "2048 1" "2048 0"; do set -- $cfg
+             PCM_TILE_CAP=$1 PCM_TILE_LPT=$2 timeout -k 10 200 python bench.py --slab-of 8 --steps 20 --warmup 3 > $T/s8_$1_$2_$r.json 2>&1 || { tail -5 $T/s8_$1_$2_$r.json; exit 1; }
+             line "cap $1 lpt $2" $T/s8_$1_$2_$r.json "'us/rank', round(d['value'],1), 'assign max', max(d['per_rank_us']['assign']), 'tiles', d['slabs'][0]['ntiles'], 'bitwise', d['centres_bitwise_equal_single_engine']"
+           done; done ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
