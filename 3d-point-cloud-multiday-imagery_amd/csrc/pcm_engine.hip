@@ -958,12 +958,17 @@ static int launch_tile_lists(pcm_engine *e, hipStream_t s, int gate) {
 
 // Persistent grid: as many 256-thread blocks as are co-resident (occupancy
 // query), never more blocks than tiles.
+// k_label's grid: one block per tile (round 6: 247-249 -> 235-237 us per final
+// E-step at config 3 against the co-resident persistent grid, as k_lloyd1
+// measured in round 2; profiles/rd6_klabel_grid_ab.txt).  PCM_ASSIGN_BLOCKS_PER_CU
+// (A/B) restores a persistent grid of that many blocks per CU.
 static int assign_grid(pcm_engine *e, const void *kern, size_t lds) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, TPB, lds) != hipSuccess || per_cu < 1)
-        per_cu = 2;
-    if (const char *ov = std::getenv("PCM_ASSIGN_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(ov));
-    return (int)std::max(1LL, std::min<long long>(e->ntiles >= 0 ? e->ntiles : e->ntiles_cap, (long long)per_cu * e->num_cu));
+    (void)kern;
+    (void)lds;
+    const long long nt = e->ntiles >= 0 ? e->ntiles : e->ntiles_cap;
+    if (const char *ov = std::getenv("PCM_ASSIGN_BLOCKS_PER_CU"))
+        return (int)std::max(1LL, std::min<long long>(nt, (long long)std::max(1, std::atoi(ov)) * e->num_cu));
+    return (int)std::max(1LL, nt);
 }
 
 static int lloyd_slots(const pcm_engine *e) {

@@ -1528,7 +1528,8 @@ __global__ void k_inert_fold(unsigned long long *__restrict__ rep, unsigned long
 
 // E-step with the current centres writing labels (sorted order) and the
 // inertia (final E-step of _kmeans.py:736-750, relocation keys).  Not gated.
-// Same tiles and candidate lists as k_lloyd1 (persistent blocks); 4 points per lane per round,
+// Same tiles and candidate lists as k_lloyd1 (blocks walk tiles b, b + G, ...;
+// the engine launches one block per tile); 4 points per lane per round,
 // the loads of the next round in flight while one is computed; compressed
 // tiles read their 8-B records (round 4), like k_lloyd1.
 template <typename T, int D, typename LT>
