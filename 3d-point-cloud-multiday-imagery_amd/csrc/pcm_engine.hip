@@ -859,11 +859,19 @@ int pcm_fit_begin(pcm_engine *e, const float *C0, double tol, int max_iter, void
     HIPCHK(hipMemsetAsync(e->lab, 0xff, (size_t)e->npad * lsize(e), s));   // "no label yet" (-1 / 0xffff)
     // previous raw statistics := 0: iteration 0 "converges" only for an empty cloud,
     // as sklearn's labels-vs-(-1) comparison does
-    HIPCHK(hipMemsetAsync(e->prev, 0, ((size_t)e->k * (e->d + 1) + 1) * sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(e->partials, 0, (size_t)2 * e->k * (e->d + 1) * sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(e->stats, 0, ((size_t)e->k * (e->d + 1) + 1) * sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(e->hist_changed, 0, (size_t)e->max_iter_cap * sizeof(unsigned long long), s));
-    HIPCHK(hipMemsetAsync(e->hist_shift, 0, (size_t)e->max_iter_cap * sizeof(double), s));
+    {   // prev, partials, stats and the histories := 0 in one launch (five memsets: ~5 us each)
+        const long long w = (long long)e->k * (e->d + 1);
+        ZeroSpans z{};
+        z.p[0] = e->prev;         z.n[0] = w + 1;
+        z.p[1] = e->partials;     z.n[1] = 2 * w;
+        z.p[2] = e->stats;        z.n[2] = w + 1;
+        z.p[3] = e->hist_changed; z.n[3] = e->max_iter_cap;
+        z.p[4] = reinterpret_cast<unsigned long long *>(e->hist_shift); z.n[4] = e->max_iter_cap;   // 0.0 = all-zero bits
+        long long tot = 0;
+        for (int q = 0; q < 5; ++q) tot += z.n[q];
+        k_zero_spans<<<(int)std::min<long long>(1024, (tot + 255) / 256), 256, 0, s>>>(z);
+        LAUNCHCHK();
+    }
     e->ctrl_host = Ctrl{};
     e->ctrl_host.max_iter = (uint32_t)max_iter;
     e->ctrl_host.tol = tol;

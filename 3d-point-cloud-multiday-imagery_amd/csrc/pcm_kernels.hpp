@@ -207,6 +207,18 @@ template <typename T> __device__ __forceinline__ float to_f(T v);
 template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ float to_f<__half>(__half v) { return __half2float(v); }
 
+// Up to 5 buffers of 64-bit words := 0 in one launch (pcm_fit_begin).
+struct ZeroSpans {
+    unsigned long long *p[5];
+    long long n[5];
+};
+__global__ __launch_bounds__(256) void k_zero_spans(ZeroSpans z) {
+    const long long st = (long long)gridDim.x * blockDim.x;
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < z.n[q]; i += st) z.p[q][i] = 0ull;
+}
+
 // ------------------------------------------------------------------ layout
 // Per-block min/max/maxabs (+ non-finite flag) of an AoS (n, D) array.
 template <typename T, int D>
