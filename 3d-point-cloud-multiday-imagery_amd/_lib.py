@@ -27,7 +27,7 @@ EXPORTS = [
     "pcm_abi_version", "pcm_last_error", "pcm_engine_create", "pcm_engine_destroy", "pcm_layout_bbox",
     "pcm_layout_build", "pcm_fit_begin", "pcm_iter_local", "pcm_iter_global", "pcm_iterate", "pcm_stats_ptr",
     "pcm_bind_stats", "pcm_reloc_candidates", "pcm_reloc_apply", "pcm_final", "pcm_labels", "pcm_get_centers",
-    "pcm_history", "pcm_read_status", "pcm_layout_info", "pcm_candidate_stats", "pcm_tile_list_stats", "pcm_tile_list_detail", "pcm_synth_uniform",
+    "pcm_history", "pcm_read_status", "pcm_status_post", "pcm_status_wait", "pcm_layout_info", "pcm_candidate_stats", "pcm_tile_list_stats", "pcm_tile_list_detail", "pcm_synth_uniform",
     "pcm_assign_bruteforce", "pcm_timing", "pcm_timing_read", "pcm_time_assign", "pcm_synth_rows", "pcm_kmeanspp", "pcm_cloud_assemble",
     "pcm_inertia_value", "pcm_kmeanspp_workspace",
     "pcm_dense_create", "pcm_dense_destroy", "pcm_dense_begin", "pcm_dense_iterate", "pcm_dense_final",
@@ -38,7 +38,7 @@ EXPORTS = [
     "pcm_xchg_create", "pcm_xchg_destroy", "pcm_xchg_handle", "pcm_xchg_open", "pcm_xchg_link", "pcm_xchg_allreduce",
     "pcm_xchg_status", "pcm_iter_exchange",
 ]
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lock = threading.Lock()
 _lib = None
@@ -129,6 +129,8 @@ def _declare(lib):
         "pcm_get_centers": ([P, P, P], I),
         "pcm_history": ([P, P, P, I, P], I),
         "pcm_read_status": ([P, ctypes.POINTER(PcmStatus), P], I),
+        "pcm_status_post": ([P, P], I),
+        "pcm_status_wait": ([P, ctypes.POINTER(PcmStatus)], I),
         "pcm_layout_info": ([P, ctypes.POINTER(I64), ctypes.POINTER(I64), P], I),
         "pcm_candidate_stats": ([P, ctypes.POINTER(D), ctypes.POINTER(I), ctypes.POINTER(I64), P], I),
         "pcm_tile_list_stats": ([P, ctypes.POINTER(I), ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(I64), P],

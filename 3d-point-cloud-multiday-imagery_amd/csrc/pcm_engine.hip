@@ -61,6 +61,8 @@ struct pcm_engine {
     long long ntiles_cap = 0;        // upper bound on the tiles of the current layout (grid sizing)
     uint32_t tile_cap = TILE;        // points per tile
     uint32_t *ntiles_host = nullptr; // pinned: the layout's tile count, read back at the end of pcm_layout_build
+    Ctrl *ctrl_pin = nullptr;        // pinned snapshot of ctrl (pcm_status_post / pcm_status_wait)
+    hipEvent_t st_ev = nullptr;
     // device buffers (persistent: grown on demand, reused by later layouts, freed at destroy)
     void *xs = nullptr;
     unsigned *xz = nullptr;          // compressed 8-B point records (fp32 D = 3, k_tile_compress)
@@ -455,6 +457,8 @@ int pcm_engine_create(int device, int d, int k, int dtype, int max_iter, pcm_eng
     err = err ? err : hipMalloc(&e->ntiles_dev, 2 * sizeof(uint32_t));
     err = err ? err : hipMalloc(&e->zpts, 32 * 16 * sizeof(unsigned long long));
     err = err ? err : hipHostMalloc((void **)&e->ntiles_host, sizeof(uint32_t), hipHostMallocDefault);
+    err = err ? err : hipHostMalloc((void **)&e->ctrl_pin, sizeof(Ctrl), hipHostMallocDefault);
+    err = err ? err : hipEventCreateWithFlags(&e->st_ev, hipEventDisableTiming);
     err = err ? err : hipMemset(e->partials, 0, (size_t)2 * k * (d + 1) * sizeof(unsigned long long));
     err = err ? err : hipMemset(e->ctrl, 0, sizeof(Ctrl));
     if (err != hipSuccess) {
@@ -481,6 +485,8 @@ int pcm_engine_destroy(pcm_engine *e) {
     for (void *p : ps)
         if (p) (void)hipFree(p);
     if (e->ntiles_host) (void)hipHostFree(e->ntiles_host);
+    if (e->ctrl_pin) (void)hipHostFree(e->ctrl_pin);
+    if (e->st_ev) (void)hipEventDestroy(e->st_ev);
     delete e;
     return 0;
 }
@@ -1500,12 +1506,7 @@ int pcm_history(pcm_engine *e, uint64_t *changed, double *shift, int cap, void *
     return 0;
 }
 
-int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream) {
-    if (!e || !out) return fail(PCM_E_ARG, "bad argument");
-    hipStream_t s = (hipStream_t)stream;
-    Ctrl h{};
-    HIPCHK(hipMemcpyAsync(&h, e->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+static void status_fill(const pcm_engine *e, const Ctrl &h, pcm_status *out) {
     out->halt = h.halt;
     out->done = h.done;
     out->iter = h.iter;
@@ -1518,6 +1519,35 @@ int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream) {
     out->pad_ = 0;
     out->last_changed = h.last_changed;
     out->last_shift = h.last_shift;
+}
+
+int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream) {
+    if (!e || !out) return fail(PCM_E_ARG, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    Ctrl h{};
+    HIPCHK(hipMemcpyAsync(&h, e->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    status_fill(e, h, out);
+    return 0;
+}
+
+// Status without draining the stream: post = a snapshot of ctrl queued behind
+// the work enqueued so far (pinned copy + event); wait = until that snapshot
+// has landed.  Lets the host queue the next chunk of iterations before it
+// reads the previous chunk's status (lloyd.run), so the GPU does not idle for
+// the round trip.  One snapshot in flight per engine.
+int pcm_status_post(pcm_engine *e, void *stream) {
+    if (!e) return fail(PCM_E_ARG, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(e->ctrl_pin, e->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(e->st_ev, s));
+    return 0;
+}
+
+int pcm_status_wait(pcm_engine *e, pcm_status *out) {
+    if (!e || !out) return fail(PCM_E_ARG, "bad argument");
+    HIPCHK(hipEventSynchronize(e->st_ev));
+    status_fill(e, *e->ctrl_pin, out);
     return 0;
 }
 

@@ -147,9 +147,23 @@ class Engine:
     def iterate(self, n: int):
         _lib.check(self.lib.pcm_iterate(self.h, int(n), _stream()), "pcm_iterate")
 
+    def status_post(self):
+        """Queue a status snapshot behind the work enqueued so far (no drain)."""
+        _lib.check(self.lib.pcm_status_post(self.h, _stream()), "pcm_status_post")
+
+    def status_wait(self) -> dict:
+        """The snapshot of the last ``status_post``, once it has landed."""
+        st = _lib.PcmStatus()
+        _lib.check(self.lib.pcm_status_wait(self.h, ctypes.byref(st)), "pcm_status_wait")
+        return self._status_dict(st)
+
     def status(self) -> dict:
         st = _lib.PcmStatus()
         _lib.check(self.lib.pcm_read_status(self.h, ctypes.byref(st), _stream()), "pcm_read_status")
+        return self._status_dict(st)
+
+    @staticmethod
+    def _status_dict(st) -> dict:
         return dict(halt=st.halt, done=st.done, iter=st.iter, n_empty=st.n_empty, inertia=st.inertia,
                     last_changed=st.last_changed, last_shift=st.last_shift,
                     inertia_limbs=[int(v) for v in st.inertia_limbs], inertia_scale=int(st.inertia_scale),

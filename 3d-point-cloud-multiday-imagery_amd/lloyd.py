@@ -264,6 +264,56 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, gra
                 dist.all_reduce(engine.stats, group=group)
             engine.iter_global()
 
+    def check(st):
+        if st["done"] == XCHG_FAILED:
+            from ._lib import PcmError
+            raise PcmError("pcm_amd.lloyd: the peer statistics exchange timed out (a rank stopped pushing); "
+                           "the fit is void")
+        if st["done"] == UPD_FAILED:
+            from ._lib import PcmError
+            raise PcmError("pcm_amd.lloyd: the update's publisher timed out waiting for its list blocks; "
+                           "the fit is void")
+
+    import os
+    if world == 1 and not split and hasattr(engine, "status_post") and os.environ.get("PCM_LLOYD_PIPE", "1") != "0":
+        # One GPU: the next chunk is queued before the previous chunk's status is
+        # read (a pinned snapshot + event behind each chunk), so the GPU does not
+        # idle through the host round trip.  Iterations queued past convergence,
+        # max_iter or a halt are gated no-ops on the device (ctrl), and a gated
+        # iteration does not advance ctrl.iter, so nothing is lost or repeated.
+        queued = min(chunk, max_iter)
+        engine.iterate(queued)
+        engine.status_post()
+        while True:
+            spec = min(chunk, max_iter - queued)
+            if spec > 0:
+                engine.iterate(spec)   # queued behind the snapshot
+                queued += spec
+            st = engine.status_wait()  # the status before that chunk
+            check(st)
+            if st["halt"]:
+                # the queued chunk ran gated; the relocation follows it in stream order
+                recs = engine.reloc_candidates(int(st["n_empty"]))
+                engine.reloc_apply(recs)
+                relocs += 1
+                st = engine.status()
+                check(st)
+                if st["done"]:
+                    return st, relocs
+                queued = int(st["iter"])   # nothing in flight: count from the device
+                n = min(chunk, max_iter - queued)
+                engine.iterate(n)
+                queued += n
+                engine.status_post()
+                continue
+            if st["done"]:
+                return st, relocs
+            if spec == 0:   # every iteration was queued before the snapshot (max_iter gates the rest)
+                st = engine.status()
+                check(st)
+                return st, relocs
+            engine.status_post()   # the status after the chunk just queued
+
     while True:
         n_enq = max(1, min(chunk, max_iter - it))
         if world == 1 and not split:
@@ -288,14 +338,7 @@ def run(engine, C0, max_iter=300, tol=0.0, group=None, chunk=8, split=False, gra
         else:
             seq(n_enq)
         st = engine.status()
-        if st["done"] == XCHG_FAILED:
-            from ._lib import PcmError
-            raise PcmError("pcm_amd.lloyd: the peer statistics exchange timed out (a rank stopped pushing); "
-                           "the fit is void")
-        if st["done"] == UPD_FAILED:
-            from ._lib import PcmError
-            raise PcmError("pcm_amd.lloyd: the update's publisher timed out waiting for its list blocks; "
-                           "the fit is void")
+        check(st)
         if st["halt"]:
             recs = engine.reloc_candidates(int(st["n_empty"]))
             if world > 1:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PCM_ABI_VERSION 5
+#define PCM_ABI_VERSION 6
 
 enum pcm_dtype { PCM_F32 = 0, PCM_F16 = 1, PCM_F64 = 2 /* dense path only */ };
 
@@ -166,6 +166,12 @@ int pcm_get_centers(pcm_engine *e, float *out, void *stream);
 int pcm_history(pcm_engine *e, uint64_t *changed, double *shift, int cap, void *stream);
 /* Synchronise `stream` and copy the device status. */
 int pcm_read_status(pcm_engine *e, pcm_status *out, void *stream);
+/* The same without draining the stream (round 6): pcm_status_post queues a
+ * snapshot of the status behind the work enqueued so far; pcm_status_wait
+ * blocks until that snapshot has landed and decodes it.  One snapshot in flight
+ * per engine (a post overwrites the previous one). */
+int pcm_status_post(pcm_engine *e, void *stream);
+int pcm_status_wait(pcm_engine *e, pcm_status *out);
 
 /* Layout facts for diagnostics: cells, tiles, grid dims (host ints). */
 int pcm_layout_info(pcm_engine *e, int64_t *ncells, int64_t *ntiles, int *grid /*[4]*/);
