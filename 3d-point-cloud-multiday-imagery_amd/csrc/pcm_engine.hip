@@ -234,10 +234,10 @@ int rs_sort(const TT *X, long long n, long long npad, const Grid &g, int with_su
         const R *rin = from_x ? nullptr : (((q - 1) & 1) ? rb : ra);
         R *rout = to_xs ? nullptr : ((q & 1) ? rb : ra);
         if (from_x)
-            k_rs_count<TT, D, true><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, hist,
+            k_rs_count<TT, D, true><<<grid, RS_CTPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, hist,
                                                              sort_vec(X) & 1);
         else
-            k_rs_count<TT, D, false><<<grid, RS_TPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, hist, 0);
+            k_rs_count<TT, D, false><<<grid, RS_CTPB, 0, s>>>(X, rin, n, g, with_sub, zlev, shift, width, hist, 0);
         LAUNCHCHK();
         k_rs_colscan<<<(int)p.nseg, RS_DIG, 0, s>>>(hist, p.nblk, goff, segb);
         LAUNCHCHK();

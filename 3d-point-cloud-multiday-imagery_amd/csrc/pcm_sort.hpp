@@ -64,15 +64,21 @@ __device__ __forceinline__ uint32_t rs_key(const PRec<T, D> &r, const Grid &g, i
     return sort_key_f<D>(x, g, with_sub, zlev);
 }
 
-// Per-chunk digit histogram.
+// Per-chunk digit histogram.  PCM_RS_CTPB: threads per count block (the
+// chunk stays RsCfg::CH items; A/B of the count's occupancy)
+#ifndef PCM_RS_CTPB
+#define PCM_RS_CTPB 512   // 256: 383 -> 512: 325 us for the record pass at config 3 (profiles/rd6_sort_count_vec.txt)
+#endif
+constexpr int RS_CTPB = PCM_RS_CTPB;
 template <typename T, int D, bool FROM_X>
-__global__ __launch_bounds__(RS_TPB) void k_rs_count(const T *__restrict__ X, const PRec<T, D> *__restrict__ rin,
+__global__ __launch_bounds__(RS_CTPB) void k_rs_count(const T *__restrict__ X, const PRec<T, D> *__restrict__ rin,
                                                      long long n, Grid g, int with_sub, int zlev, int shift, int width,
                                                      uint32_t *__restrict__ hist, int vec) {
-    constexpr int IPT = RsCfg<T, D>::IPT, CH = RsCfg<T, D>::CH;
-    __shared__ uint32_t h[RS_NWV][RS_DIG];
+    constexpr int CH = RsCfg<T, D>::CH, CNWV = RS_CTPB / 64, IPT = CH / RS_CTPB;
+    static_assert(CH % RS_CTPB == 0 && RS_CTPB >= RS_DIG, "count block geometry");
+    __shared__ uint32_t h[CNWV][RS_DIG];
     const int tid = threadIdx.x, wv = tid >> 6;
-    for (int k = tid; k < RS_NWV * RS_DIG; k += RS_TPB) (&h[0][0])[k] = 0u;
+    for (int k = tid; k < CNWV * RS_DIG; k += RS_CTPB) (&h[0][0])[k] = 0u;
     __syncthreads();
     const long long base = (long long)blockIdx.x * CH;
     const uint32_t mask = (1u << width) - 1u;
@@ -82,7 +88,7 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_count(const T *__restrict__ X, co
             float4 q[G][3];
 #pragma unroll
             for (int u = 0; u < G; ++u) {
-                const long long r0 = base + 4LL * (u * RS_TPB + tid);
+                const long long r0 = base + 4LL * (u * RS_CTPB + tid);
                 if (r0 + 3 < n) {
                     const float4 *p = reinterpret_cast<const float4 *>(X + r0 * 3);
                     q[u][0] = p[0]; q[u][1] = p[1]; q[u][2] = p[2];
@@ -90,7 +96,7 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_count(const T *__restrict__ X, co
             }
 #pragma unroll
             for (int u = 0; u < G; ++u) {
-                const long long r0 = base + 4LL * (u * RS_TPB + tid);
+                const long long r0 = base + 4LL * (u * RS_CTPB + tid);
                 if (r0 >= n) continue;
                 float f[12];
                 if (r0 + 3 < n) {
@@ -111,7 +117,7 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_count(const T *__restrict__ X, co
             if (tid < RS_DIG) {
                 uint32_t t = 0u;
 #pragma unroll
-                for (int w = 0; w < RS_NWV; ++w) t += h[w][tid];
+                for (int w = 0; w < CNWV; ++w) t += h[w][tid];
                 hist[(long long)blockIdx.x * RS_DIG + tid] = t;
             }
             return;
@@ -120,19 +126,19 @@ __global__ __launch_bounds__(RS_TPB) void k_rs_count(const T *__restrict__ X, co
     PRec<T, D> r[IPT];
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
-        const long long i = base + (long long)j * RS_TPB + tid;
+        const long long i = base + (long long)j * RS_CTPB + tid;
         if (i < n) rs_load<T, D, FROM_X>(X, rin, i, r[j]);
     }
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
-        const long long i = base + (long long)j * RS_TPB + tid;
+        const long long i = base + (long long)j * RS_CTPB + tid;
         if (i < n) atomicAdd(&h[wv][(rs_key<T, D>(r[j], g, with_sub, zlev) >> shift) & mask], 1u);
     }
     __syncthreads();
     if (tid < RS_DIG) {
         uint32_t t = 0u;
 #pragma unroll
-        for (int w = 0; w < RS_NWV; ++w) t += h[w][tid];
+        for (int w = 0; w < CNWV; ++w) t += h[w][tid];
         hist[(long long)blockIdx.x * RS_DIG + tid] = t;   // chunk-major: one coalesced 1-KB row per chunk
     }
 }
