@@ -24,9 +24,9 @@
 namespace pcm {
 
 #ifndef PCM_RS_TPB
-#define PCM_RS_TPB 256
+#define PCM_RS_TPB 512   // 256: scatters 885 / 975 us, 512: 652 / 799 us at config 3 (profiles/rd6_sort_tpb512.txt)
 #endif
-constexpr int RS_TPB = PCM_RS_TPB;   // threads per sort block (256 or 512)
+constexpr int RS_TPB = PCM_RS_TPB;   // threads per scatter block (256 or 512; chunks stay RsCfg::CH items)
 constexpr int RS_NWV = RS_TPB / 64;
 constexpr int RS_DIG = 256;          // digit values per pass (<= 8 bits)
 
@@ -35,8 +35,8 @@ template <typename T, int D> struct RsCfg {
     // chunks give longer output runs per digit: 4096 items measured 858 / 1185 us for the two
     // config-3 scatters, 3072 (with a 4-B key staged and written per item) 1376 / 2084 us,
     // 2048 slower overall (layout 5.37 vs 4.95 ms)
-    static constexpr int IPT = sizeof(PRec<T, D>) <= 16 ? 16 : 12;
-    static constexpr int CH = RS_TPB * IPT;   // items per chunk
+    static constexpr int CH = sizeof(PRec<T, D>) <= 16 ? 4096 : 3072;   // items per chunk
+    static constexpr int IPT = CH / RS_TPB;                               // (16 / 12 at 256 threads)
 };
 
 // Item i of a pass: the first pass reads the caller's row i, later passes the
